@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark of the reference's hot path on MI355X: candidate renders/s.
+
+Workload (BASELINE.json `metric`, configs[1]): 512x512 canvas, 256 splats per
+candidate, pop = 128 candidates per GPU, weighted-L2 fitness (the GA's default
+path, fitness.py:28-31 with the importance mask) — one *step* = one generation's
+evaluation: encode + preprocess + raster + fused weighted L2 + finalize for all
+128 candidates (libggs.so, device-pointer API, inputs resident in HBM), plus —
+for N > 1 GPUs — the RCCL all-gather of the fitness scalars (the only exchange
+step; candidates are sharded, weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  Synthetic data: genomes drawn from the
+population.py:20-46 distributions (4 different populations resident in HBM,
+cycled step to step), target U[0,1], mask U[0.405,1].
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "genetic-gaussian-splats_amd"))
+
+H = W = 512
+N_SPLATS = 256
+POP = 128
+K_SIGMA = 3.0
+N_POPS = 4
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: peak FP32 vector
+FLOP_PER_PAIR = 24
+# algorithmic bytes per candidate, fused fitness = 12HW + 4HW + 36N + 4
+BYTES_PER_CANDIDATE = 12 * H * W + 4 * H * W + 36 * N_SPLATS + 4
+
+
+def synthetic_population(B, N, seed):
+    """population.py:20-46 distributions (numpy RNG)."""
+    rng = np.random.default_rng(seed)
+    s_lo, s_hi = 3.0, 0.1 * max(H, W)
+
+    def log_scales(m):
+        u = rng.beta(m * 8 + 1e-6, (1 - m) * 8 + 1e-6, size=(B, N, 1))
+        return np.log(s_lo + u * (s_hi - s_lo))
+
+    G = np.concatenate([rng.uniform(0, 1, (B, N, 2)), log_scales(0.4), log_scales(0.6),
+                        rng.uniform(-np.pi, np.pi, (B, N, 1)), rng.uniform(0, 256, (B, N, 3)),
+                        rng.uniform(180, 256, (B, N, 1))], -1).astype(np.float32)
+    G[..., 5:9] = np.clip(G[..., 5:9], 0, 255)
+    return G
+
+
+def _cpu_worker(args):
+    pop, tgt, mask = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import ggs_oracle as O
+    return O.fitness_many(list(pop), tgt, H, W, K_SIGMA, weight_mask=mask)
+
+
+def cpu_baseline(tgt, mask, per_worker=6):
+    """The oracle (numpy restatement of render.py + fitness.py) timed on the
+    host cores, candidates split over a process pool.  Runs BEFORE any GPU
+    initialisation (fork)."""
+    import multiprocessing as mp
+    cores = max(1, min(16, os.cpu_count() or 1))
+    pops = [synthetic_population(per_worker, N_SPLATS, 1000 + i) for i in range(cores)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(cores) as pool:
+        pool.map(_cpu_worker, [(p[:1], tgt, mask) for p in pops])     # warm the workers
+        t0 = time.perf_counter()
+        pool.map(_cpu_worker, [(p, tgt, mask) for p in pops])
+        dt = time.perf_counter() - t0
+    n = cores * per_worker
+    return {"value": n / dt, "unit": "candidate renders/s", "cores": cores, "kind": "port",
+            "sample": f"{n} candidates ({per_worker} per process x {cores} processes, 1 thread each) "
+                      f"at 512x512/256 splats, weighted fitness, oracle/ggs_oracle.py numpy; {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    rng = np.random.default_rng(1234)
+    tgt_h = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask_h = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(tgt_h, mask_h)
+
+    import torch
+    import torch.distributed as dist
+    import ggs
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    pops = [torch.from_numpy(synthetic_population(POP, N_SPLATS, 10_000 * rank + i)).to(dev)
+            for i in range(N_POPS)]
+    tgt = torch.from_numpy(tgt_h).to(dev)
+    mask = torch.from_numpy(mask_h).to(dev)
+    out = torch.empty(POP, dtype=torch.float32, device=dev)
+    gathered = torch.empty(POP * world, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    st = stream.cuda_stream
+
+    def step(i):
+        g = pops[i % N_POPS]
+        ggs.fitness_device(local_rank, st, g.data_ptr(), POP, N_SPLATS, 9, tgt.data_ptr(),
+                           mask.data_ptr(), ggs.GGS_FIT_WEIGHTED, 1.0, H, W, K_SIGMA, out.data_ptr())
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)      # RCCL: fitness scalars to every rank
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel device time (HIP events on the launch stream) over a second,
+    # identical pass; the raster kernel is the dominant one
+    ggs.profile_reset()
+    ggs.profile_enable(True)
+    for i in range(args.steps):
+        step(i)
+    barrier()
+    ggs.profile_enable(False)
+    kern = {k: ggs.profile_read(k) for k in ("prep", "raster", "finalize")}
+    raster_ms = kern["raster"][0] / max(kern["raster"][1], 1)
+
+    # algorithmic work of this workload (AABB pairs from the product's own prep)
+    pairs = 0
+    for p in pops:
+        pre = ggs.preprocess(ggs.encode(p.cpu().numpy()), H, W, K_SIGMA)
+        pairs += int(((pre["x1"].astype(np.int64) - pre["x0"] + 1) *
+                      (pre["y1"].astype(np.int64) - pre["y0"] + 1)).sum())
+    pairs_per_cand = pairs / (N_POPS * POP)
+
+    total = world * POP * args.steps
+    value = total / elapsed
+    raster_bytes = BYTES_PER_CANDIDATE * POP
+    achieved_gbs = raster_bytes / (raster_ms * 1e-3) / 1e9
+    valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
+    if rank == 0:
+        line = {
+            "metric": "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=128",
+            "value": round(value, 1),
+            "unit": "candidate renders/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (population.py distributions, U[0,1] target, U[0.405,1] mask)",
+            "config": {"workload": "512x512 canvas, 256 splats/candidate, pop=128 per GPU, "
+                                   "weighted-L2 fitness (encode+prep+raster+reduce)",
+                       "H": H, "W": W, "splats": N_SPLATS, "pop_per_gpu": POP,
+                       "global_batch": POP * world, "parallelism": f"dp{world} (candidate shards)"},
+            "gsplat_pixels_per_s": round(value * N_SPLATS * H * W / 1e9, 2),
+            "aabb_pairs_per_s": round(value * pairs_per_cand, 1),
+            "roofline": {"bound": "hbm", "kernel": "raster_kernel<2>",
+                         "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": None,
+                         "algorithmic_bytes_per_launch": raster_bytes,
+                         "avg_launch_ms": round(raster_ms, 5),
+                         "note": "VALU/transcendental-bound path (SURVEY.md §8d): see 'valu'"},
+            "valu": {"achieved": round(valu_tflops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
+                     "flop_per_aabb_pair": FLOP_PER_PAIR, "aabb_pairs_per_candidate": pairs_per_cand},
+            "kernels_ms_per_launch": {k: round(v[0] / max(v[1], 1), 5) for k, v in kern.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,615 @@
+// C-ABI of libggs.so (declared in include/ggs.h): device contexts, pooled
+// workspaces, host<->device staging, multi-device fan-out, error reporting and
+// per-kernel event timing.  The kernels live in ggs_kernels.hip.
+//
+// Reference boundary replaced here:
+//   render_splats_rgb_triton  modules/render.py:203-252  -> ggs_render / ggs_render_device
+//   fitness_many              modules/fitness.py:7-31    -> ggs_fitness / ggs_fitness_device
+//   (fitness_population fitness.py:34-47 and the list/tensor plumbing stay in Python)
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ggs_internal.h"
+
+namespace ggs {
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return code;
+}
+
+#define GGS_HIP(call)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (call);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail(e_ == hipErrorOutOfMemory ? GGS_ENOMEM : GGS_EHIP, "%s: %s (%s:%d)",     \
+                        #call, hipGetErrorString(e_), __FILE__, __LINE__);                       \
+    } while (0)
+
+// ---- device buffers ---------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+// Grow `b` to at least `bytes`.  `st` is the stream that may still be using the
+// old allocation; it is synchronised before the free.
+int ensure(DevBuf& b, size_t bytes, hipStream_t st) {
+    if (bytes <= b.cap) return GGS_OK;
+    if (b.p) {
+        GGS_HIP(hipStreamSynchronize(st));
+        GGS_HIP(hipFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+    GGS_HIP(hipMalloc(&b.p, want));
+    b.cap = want;
+    return GGS_OK;
+}
+
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+int ensure_pinned(PinBuf& b, size_t bytes) {
+    if (bytes <= b.cap) return GGS_OK;
+    if (b.p) {
+        GGS_HIP(hipHostFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+    GGS_HIP(hipHostMalloc(&b.p, want, hipHostMallocDefault));
+    b.cap = want;
+    return GGS_OK;
+}
+
+// Per-(device, stream) scratch used by one render/fitness pipeline.
+struct Workspace {
+    hipStream_t stream = nullptr;
+    DevBuf recs, partials, wpartials;
+};
+
+struct DevCtx {
+    int dev = 0;
+    hipStream_t stream = nullptr;  // library-owned stream for the host API
+    std::mutex mu;
+    std::vector<std::unique_ptr<Workspace>> ws;
+    // host-API staging
+    DevBuf gen, out, target, mask;
+    PinBuf h_gen, h_out;
+    uint64_t target_key = 0, mask_key = 0;
+    size_t target_bytes = 0, mask_bytes = 0;
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<DevCtx>> g_ctx;  // indexed by HIP device id
+std::vector<int> g_active;                    // devices the host API fans out over
+bool g_inited = false;
+
+// ---- profiling ----------------------------------------------------------------
+struct ProfRec {
+    int kernel;  // 0 prep, 1 raster, 2 finalize
+    hipEvent_t a, b;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_prof_pending;
+double g_prof_ms[3] = {0, 0, 0};
+int64_t g_prof_n[3] = {0, 0, 0};
+const char* const kKernelNames[3] = {"prep", "raster", "finalize"};
+
+struct ProfScope {
+    bool on = false;
+    hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t st;
+    int kernel;
+    ProfScope(hipStream_t s, int k) : st(s), kernel(k) {
+        {
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            on = g_prof_on;
+        }
+        if (on && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+            (void)hipEventRecord(a, st);
+        else
+            on = false;
+    }
+    ~ProfScope() {
+        if (!on) return;
+        (void)hipEventRecord(b, st);
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof_pending.push_back({kernel, a, b});
+    }
+};
+
+void prof_drain_locked() {
+    for (auto& r : g_prof_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_prof_ms[r.kernel] += ms;
+            g_prof_n[r.kernel] += 1;
+        }
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    g_prof_pending.clear();
+}
+
+// ---- helpers ----------------------------------------------------------------------
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int init_locked(int max_devices) {
+    if (g_inited) return (int)g_ctx.size();
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        return fail(GGS_ENODEV, "no HIP device available (%s); the reference asserts a GPU too "
+                                "(render.py:217)", e != hipSuccess ? hipGetErrorString(e) : "count=0");
+    if (max_devices > 0) n = std::min(n, max_devices);
+    g_ctx.resize(n);              // contexts are created on first use (ctx_locked)
+    g_active.clear();
+    for (int d = 0; d < n; ++d) g_active.push_back(d);
+    g_inited = true;
+    return n;
+}
+
+int lazy_init() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_locked(0);
+}
+
+// Context of device d, created on first use (one stream per device).  g_mu held.
+int ctx_locked(int d, DevCtx** out) {
+    if (d < 0 || d >= (int)g_ctx.size())
+        return fail(GGS_EINVAL, "device %d out of range (have %d)", d, (int)g_ctx.size());
+    if (!g_ctx[d]) {
+        auto c = std::make_unique<DevCtx>();
+        c->dev = d;
+        DeviceGuard dg(d);
+        GGS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        g_ctx[d] = std::move(c);
+    }
+    *out = g_ctx[d].get();
+    return GGS_OK;
+}
+
+int get_ctx(int device, DevCtx** out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int rc = init_locked(0);
+    if (rc < 0) return rc;
+    return ctx_locked(device, out);
+}
+
+// The first n (<=0: all) devices of the active list, contexts created.
+int active_ctxs(int32_t n_devices, std::vector<DevCtx*>* out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int rc = init_locked(0);
+    if (rc < 0) return rc;
+    const int have = (int)g_active.size();
+    const int n = n_devices <= 0 ? have : std::min<int>(n_devices, have);
+    out->clear();
+    for (int i = 0; i < n; ++i) {
+        DevCtx* c;
+        if ((rc = ctx_locked(g_active[i], &c))) return rc;
+        out->push_back(c);
+    }
+    return GGS_OK;
+}
+
+Workspace* workspace_for(DevCtx* c, hipStream_t st) {
+    for (auto& w : c->ws)
+        if (w->stream == st) return w.get();
+    c->ws.push_back(std::make_unique<Workspace>());
+    c->ws.back()->stream = st;
+    return c->ws.back().get();
+}
+
+// xxhash64-style content hash (target/mask upload cache)
+inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+uint64_t hash_bytes(const void* data, size_t n) {
+    const uint64_t P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull;
+    const unsigned char* p = (const unsigned char*)data;
+    uint64_t v[4] = {P1 + P2, P2, 0, 0 - P1};
+    size_t i = 0;
+    for (; i + 32 <= n; i += 32) {
+        for (int k = 0; k < 4; ++k) {
+            uint64_t w;
+            memcpy(&w, p + i + 8 * k, 8);
+            v[k] = rotl(v[k] + w * P2, 31) * P1;
+        }
+    }
+    uint64_t h = rotl(v[0], 1) + rotl(v[1], 7) + rotl(v[2], 12) + rotl(v[3], 18) + n;
+    for (; i < n; ++i) h = rotl(h ^ (p[i] * P3), 11) * P1;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
+}
+
+int check_dims(int64_t B, int32_t N, int32_t C, int32_t H, int32_t W) {
+    if (B < 0 || N < 0) return fail(GGS_EINVAL, "B=%lld and N=%d must be >= 0", (long long)B, N);
+    if (C < 9) return fail(GGS_EINVAL, "expected at least 9 genome cols, got C=%d (render.py:223)", C);
+    if (H < 1 || W < 1) return fail(GGS_EINVAL, "H=%d, W=%d must be >= 1", H, W);
+    int nTX;
+    const int64_t nTiles = raster_tiles(H, W, &nTX);
+    if (B * nTiles >= (int64_t)1 << 31)
+        return fail(GGS_EINVAL, "B*tiles = %lld exceeds the grid limit; split the batch",
+                    (long long)(B * nTiles));
+    return GGS_OK;
+}
+
+// ---- the device pipelines (ctx locked, device set) ----------------------------------
+int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, int C,
+                const float* d_target, const float* d_mask, int mode, float beta, int H, int W,
+                float k, float* d_out) {
+    if (B == 0) return GGS_OK;
+    Workspace* w = workspace_for(c, st);
+    int nTX;
+    const int nTiles = raster_tiles(H, W, &nTX);
+    int rc;
+    if ((rc = ensure(w->recs, sizeof(SplatRec) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
+    if ((rc = ensure(w->partials, sizeof(float) * (size_t)(B * nTiles), st))) return rc;
+    if ((rc = ensure(w->wpartials, sizeof(float) * (size_t)nTiles, st))) return rc;
+    SplatRec* recs = (SplatRec*)w->recs.p;
+    {
+        ProfScope ps(st, 0);
+        GGS_HIP(launch_prep(st, true, d_gen, B * N, C, H, W, k, recs, nullptr, nullptr, nullptr));
+    }
+    const float bg[3] = {1.f, 1.f, 1.f};  // fitness renders with the default background (fitness.py:15)
+    {
+        ProfScope ps(st, 1);
+        GGS_HIP(launch_raster(st, 1 + mode, recs, (int)B, N, H, W, bg, nullptr, d_target, d_mask, beta,
+                              (float*)w->partials.p, (float*)w->wpartials.p));
+    }
+    {
+        ProfScope ps(st, 2);
+        GGS_HIP(launch_finalize(st, (const float*)w->partials.p, (const float*)w->wpartials.p, (int)B,
+                                nTiles, mode, H, W, d_out));
+    }
+    return GGS_OK;
+}
+
+int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, int C, int H, int W,
+               float k, const float bg[3], float* d_img) {
+    if (B == 0) return GGS_OK;
+    Workspace* w = workspace_for(c, st);
+    int rc;
+    if ((rc = ensure(w->recs, sizeof(SplatRec) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
+    SplatRec* recs = (SplatRec*)w->recs.p;
+    {
+        ProfScope ps(st, 0);
+        GGS_HIP(launch_prep(st, false, d_gen, B * N, C, H, W, k, recs, nullptr, nullptr, nullptr));
+    }
+    {
+        ProfScope ps(st, 1);
+        GGS_HIP(launch_raster(st, 0, recs, (int)B, N, H, W, bg, d_img, nullptr, nullptr, 0.f, nullptr,
+                              nullptr));
+    }
+    return GGS_OK;
+}
+
+// Split [0, B) into n contiguous shards.
+void shard(int64_t B, int n, int d, int64_t* b0, int64_t* nb) {
+    const int64_t base = B / n, rem = B % n;
+    *b0 = d * base + std::min<int64_t>(d, rem);
+    *nb = base + (d < rem ? 1 : 0);
+}
+
+}  // namespace
+}  // namespace ggs
+
+using namespace ggs;
+
+extern "C" {
+
+const char* ggs_version(void) { return "ggs-mi355x 0.1.0 (gfx950)"; }
+
+int ggs_init(int32_t max_devices) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_locked(max_devices);
+}
+
+int ggs_device_count(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_inited ? (int)g_ctx.size() : 0;
+}
+
+int ggs_select_devices(const int32_t* ids, int32_t n) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int rc = init_locked(0);
+    if (rc < 0) return rc;
+    if (n < 0 || (n > 0 && !ids)) return fail(GGS_EINVAL, "bad device list");
+    std::vector<int> act;
+    for (int i = 0; i < n; ++i) {
+        if (ids[i] < 0 || ids[i] >= (int)g_ctx.size())
+            return fail(GGS_EINVAL, "device %d out of range (have %d)", ids[i], (int)g_ctx.size());
+        if (std::find(act.begin(), act.end(), ids[i]) != act.end())
+            return fail(GGS_EINVAL, "device %d listed twice", ids[i]);
+        act.push_back(ids[i]);
+    }
+    if (act.empty())
+        for (int d = 0; d < (int)g_ctx.size(); ++d) act.push_back(d);
+    g_active = act;
+    return (int)g_active.size();
+}
+
+const char* ggs_last_error(void) { return t_err.c_str(); }
+
+void ggs_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    {
+        std::lock_guard<std::mutex> pl(g_prof_mu);
+        prof_drain_locked();
+    }
+    for (auto& c : g_ctx) {
+        if (!c) continue;
+        std::lock_guard<std::mutex> cl(c->mu);
+        (void)hipSetDevice(c->dev);
+        (void)hipStreamSynchronize(c->stream);
+        for (auto& w : c->ws) {
+            if (w->stream) (void)hipStreamSynchronize(w->stream);
+            for (DevBuf* b : {&w->recs, &w->partials, &w->wpartials})
+                if (b->p) (void)hipFree(b->p);
+        }
+        for (DevBuf* b : {&c->gen, &c->out, &c->target, &c->mask})
+            if (b->p) (void)hipFree(b->p);
+        for (PinBuf* b : {&c->h_gen, &c->h_out})
+            if (b->p) (void)hipHostFree(b->p);
+        (void)hipStreamDestroy(c->stream);
+    }
+    g_ctx.clear();
+    g_active.clear();
+    g_inited = false;
+}
+
+int ggs_fitness_device(int32_t device, void* stream, const float* d_genomes_axes, int64_t B, int32_t N,
+                       int32_t C, const float* d_target_hw3, const float* d_mask_hw, int32_t mode,
+                       float boost_beta, int32_t H, int32_t W, float k_sigma, float* d_out_B) {
+    int rc = check_dims(B, N, C, H, W);
+    if (rc) return rc;
+    if (mode < GGS_FIT_NONE || mode > GGS_FIT_BOOST) return fail(GGS_EINVAL, "bad fitness mode %d", mode);
+    if (mode != GGS_FIT_NONE && !d_mask_hw) return fail(GGS_EINVAL, "mode %d needs a weight mask", mode);
+    if (B > 0 && (!d_genomes_axes && N > 0)) return fail(GGS_EINVAL, "null genomes");
+    if (B > 0 && (!d_target_hw3 || !d_out_B)) return fail(GGS_EINVAL, "null target/out");
+    DevCtx* c = nullptr;
+    if ((rc = get_ctx(device, &c))) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->dev);
+    return run_fitness(c, (hipStream_t)stream, d_genomes_axes, B, N, C, d_target_hw3, d_mask_hw, mode,
+                       boost_beta, H, W, k_sigma, d_out_B);
+}
+
+int ggs_render_device(int32_t device, void* stream, const float* d_genomes, int64_t B, int32_t N,
+                      int32_t C, int32_t H, int32_t W, float k_sigma, const float* bg,
+                      float* d_out_bhw3) {
+    int rc = check_dims(B, N, C, H, W);
+    if (rc) return rc;
+    if (B > 0 && ((!d_genomes && N > 0) || !d_out_bhw3)) return fail(GGS_EINVAL, "null pointer");
+    DevCtx* c = nullptr;
+    if ((rc = get_ctx(device, &c))) return rc;
+    const float bg1[3] = {1.f, 1.f, 1.f};
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->dev);
+    return run_render(c, (hipStream_t)stream, d_genomes, B, N, C, H, W, k_sigma, bg ? bg : bg1, d_out_bhw3);
+}
+
+int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, const float* target_hw3,
+                const float* mask_hw, int32_t mode, float boost_beta, int32_t H, int32_t W,
+                float k_sigma, float* out_B, int32_t n_devices) {
+    int rc = check_dims(B, N, C, H, W);
+    if (rc) return rc;
+    if (mode < GGS_FIT_NONE || mode > GGS_FIT_BOOST) return fail(GGS_EINVAL, "bad fitness mode %d", mode);
+    if (mode != GGS_FIT_NONE && !mask_hw) return fail(GGS_EINVAL, "mode %d needs a weight mask", mode);
+    if (B == 0) return GGS_OK;
+    if ((!genomes_axes && N > 0) || !target_hw3 || !out_B) return fail(GGS_EINVAL, "null pointer");
+    std::vector<DevCtx*> cs;
+    if ((rc = active_ctxs(n_devices, &cs))) return rc;
+    const int nd = (int)cs.size();
+    const size_t tbytes = sizeof(float) * 3 * (size_t)H * W, mbytes = sizeof(float) * (size_t)H * W;
+    const uint64_t tkey = hash_bytes(target_hw3, tbytes);
+    const uint64_t mkey = mask_hw ? hash_bytes(mask_hw, mbytes) : 0;
+    const size_t row = (size_t)N * C;
+
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (int d = 0; d < nd; ++d) locks.emplace_back(cs[d]->mu);
+    // enqueue on every device, then wait on every device
+    for (int d = 0; d < nd; ++d) {
+        DevCtx* c = cs[d];
+        int64_t b0, nb;
+        shard(B, nd, d, &b0, &nb);
+        if (nb == 0) continue;
+        DeviceGuard dg(c->dev);
+        hipStream_t st = c->stream;
+        if ((rc = ensure(c->target, tbytes, st))) return rc;
+        if (tkey != c->target_key || tbytes != c->target_bytes) {
+            GGS_HIP(hipMemcpyAsync(c->target.p, target_hw3, tbytes, hipMemcpyHostToDevice, st));
+            c->target_key = tkey;
+            c->target_bytes = tbytes;
+        }
+        if (mask_hw) {
+            if ((rc = ensure(c->mask, mbytes, st))) return rc;
+            if (mkey != c->mask_key || mbytes != c->mask_bytes) {
+                GGS_HIP(hipMemcpyAsync(c->mask.p, mask_hw, mbytes, hipMemcpyHostToDevice, st));
+                c->mask_key = mkey;
+                c->mask_bytes = mbytes;
+            }
+        }
+        const size_t gbytes = sizeof(float) * row * (size_t)nb;
+        if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
+        if ((rc = ensure(c->out, sizeof(float) * nb, st))) return rc;
+        if ((rc = ensure_pinned(c->h_gen, std::max<size_t>(gbytes, 4)))) return rc;
+        if ((rc = ensure_pinned(c->h_out, sizeof(float) * nb))) return rc;
+        GGS_HIP(hipStreamSynchronize(st));  // pinned staging may still feed a previous copy
+        if (gbytes) {
+            memcpy(c->h_gen.p, genomes_axes + row * b0, gbytes);
+            GGS_HIP(hipMemcpyAsync(c->gen.p, c->h_gen.p, gbytes, hipMemcpyHostToDevice, st));
+        }
+        if ((rc = run_fitness(c, st, (const float*)c->gen.p, nb, N, C, (const float*)c->target.p,
+                              mask_hw ? (const float*)c->mask.p : nullptr, mode, boost_beta, H, W,
+                              k_sigma, (float*)c->out.p)))
+            return rc;
+        GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, sizeof(float) * nb, hipMemcpyDeviceToHost, st));
+    }
+    for (int d = 0; d < nd; ++d) {
+        DevCtx* c = cs[d];
+        int64_t b0, nb;
+        shard(B, nd, d, &b0, &nb);
+        if (nb == 0) continue;
+        DeviceGuard dg(c->dev);
+        GGS_HIP(hipStreamSynchronize(c->stream));
+        memcpy(out_B + b0, c->h_out.p, sizeof(float) * nb);
+    }
+    return GGS_OK;
+}
+
+int ggs_render(const float* genomes, int64_t B, int32_t N, int32_t C, int32_t H, int32_t W,
+               float k_sigma, const float* bg, float* out_bhw3, int32_t n_devices) {
+    int rc = check_dims(B, N, C, H, W);
+    if (rc) return rc;
+    if (B == 0) return GGS_OK;
+    if ((!genomes && N > 0) || !out_bhw3) return fail(GGS_EINVAL, "null pointer");
+    std::vector<DevCtx*> cs;
+    if ((rc = active_ctxs(n_devices, &cs))) return rc;
+    const float bg1[3] = {1.f, 1.f, 1.f};
+    const float* bgp = bg ? bg : bg1;
+    const int nd = (int)cs.size();
+    const size_t row = (size_t)N * C;
+    const size_t img1 = sizeof(float) * 3 * (size_t)H * W;
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (int d = 0; d < nd; ++d) locks.emplace_back(cs[d]->mu);
+    for (int d = 0; d < nd; ++d) {
+        DevCtx* c = cs[d];
+        int64_t b0, nb;
+        shard(B, nd, d, &b0, &nb);
+        if (nb == 0) continue;
+        DeviceGuard dg(c->dev);
+        hipStream_t st = c->stream;
+        const size_t gbytes = sizeof(float) * row * (size_t)nb;
+        if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
+        if ((rc = ensure(c->out, img1 * nb, st))) return rc;
+        if ((rc = ensure_pinned(c->h_gen, std::max<size_t>(gbytes, 4)))) return rc;
+        if ((rc = ensure_pinned(c->h_out, img1 * nb))) return rc;
+        GGS_HIP(hipStreamSynchronize(st));
+        if (gbytes) {
+            memcpy(c->h_gen.p, genomes + row * b0, gbytes);
+            GGS_HIP(hipMemcpyAsync(c->gen.p, c->h_gen.p, gbytes, hipMemcpyHostToDevice, st));
+        }
+        if ((rc = run_render(c, st, (const float*)c->gen.p, nb, N, C, H, W, k_sigma, bgp, (float*)c->out.p)))
+            return rc;
+        GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, img1 * nb, hipMemcpyDeviceToHost, st));
+    }
+    for (int d = 0; d < nd; ++d) {
+        DevCtx* c = cs[d];
+        int64_t b0, nb;
+        shard(B, nd, d, &b0, &nb);
+        if (nb == 0) continue;
+        DeviceGuard dg(c->dev);
+        GGS_HIP(hipStreamSynchronize(c->stream));
+        memcpy((char*)out_bhw3 + img1 * b0, c->h_out.p, img1 * nb);
+    }
+    return GGS_OK;
+}
+
+static int stage_call(bool encode, const float* in, int64_t S, int32_t C, int32_t H, int32_t W, float k,
+                      float* f9, int32_t* i4, float* enc9) {
+    if (S < 0 || C < 9) return fail(GGS_EINVAL, "S=%lld must be >= 0 and C=%d >= 9", (long long)S, C);
+    if (S == 0) return GGS_OK;
+    if (!in) return fail(GGS_EINVAL, "null input");
+    int rc;
+    std::vector<DevCtx*> cs;
+    if ((rc = active_ctxs(1, &cs))) return rc;
+    DevCtx* c = cs[0];
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->dev);
+    hipStream_t st = c->stream;
+    struct Scratch {
+        void* p = nullptr;
+        ~Scratch() { if (p) (void)hipFree(p); }
+    } din, dout;
+    const size_t ib = sizeof(float) * (size_t)S * C, ob = (f9 ? 13 : 9) * sizeof(float) * (size_t)S;
+    GGS_HIP(hipMalloc(&din.p, ib));
+    GGS_HIP(hipMalloc(&dout.p, ob));
+    GGS_HIP(hipMemcpyAsync(din.p, in, ib, hipMemcpyHostToDevice, st));
+    float* o = (float*)dout.p;
+    GGS_HIP(launch_prep(st, encode, (const float*)din.p, S, C, H, W, k, nullptr, f9 ? o : nullptr,
+                        f9 ? (int*)(o + 9 * S) : nullptr, enc9 ? o : nullptr));
+    GGS_HIP(hipStreamSynchronize(st));
+    if (f9) {
+        GGS_HIP(hipMemcpy(f9, o, 9 * sizeof(float) * S, hipMemcpyDeviceToHost));
+        GGS_HIP(hipMemcpy(i4, o + 9 * S, 4 * sizeof(int) * S, hipMemcpyDeviceToHost));
+    } else {
+        GGS_HIP(hipMemcpy(enc9, o, 9 * sizeof(float) * S, hipMemcpyDeviceToHost));
+    }
+    return GGS_OK;
+}
+
+int ggs_encode(const float* genomes_axes, int64_t S, int32_t C, float* out_S9) {
+    if (!out_S9 && S > 0) return fail(GGS_EINVAL, "null output");
+    return stage_call(true, genomes_axes, S, C, 1, 1, 3.f, nullptr, nullptr, out_S9);
+}
+
+int ggs_preprocess(const float* genomes, int64_t S, int32_t C, int32_t H, int32_t W, float k_sigma,
+                   float* out_f9, int32_t* out_i4) {
+    if ((!out_f9 || !out_i4) && S > 0) return fail(GGS_EINVAL, "null output");
+    if (H < 1 || W < 1) return fail(GGS_EINVAL, "H=%d, W=%d must be >= 1", H, W);
+    return stage_call(false, genomes, S, C, H, W, k_sigma, out_f9, out_i4, nullptr);
+}
+
+int ggs_profile_enable(int32_t on) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_on = on != 0;
+    return GGS_OK;
+}
+
+int ggs_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    prof_drain_locked();
+    for (int k = 0; k < 3; ++k) {
+        if (kernel && strcmp(kernel, kKernelNames[k]) == 0) {
+            if (total_ms) *total_ms = g_prof_ms[k];
+            if (launches) *launches = g_prof_n[k];
+            return GGS_OK;
+        }
+    }
+    return fail(GGS_EINVAL, "unknown kernel name '%s' (prep|raster|finalize)", kernel ? kernel : "(null)");
+}
+
+void ggs_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    prof_drain_locked();
+    for (int k = 0; k < 3; ++k) {
+        g_prof_ms[k] = 0;
+        g_prof_n[k] = 0;
+    }
+}
+
+}  // extern "C"

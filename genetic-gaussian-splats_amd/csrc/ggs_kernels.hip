@@ -1,0 +1,388 @@
+// MI355X (gfx950) kernels for the 2D Gaussian-splat render + fitness hot path.
+//
+// Replaces, behind the reference's interfaces:
+//   encode      genome_to_renderer_batched         modules/encode.py:4-79
+//   preprocess  _preprocess_genome                 modules/render.py:8-47
+//   binning     _gpu_bin_splats_to_tiles           modules/render.py:50-118
+//   raster      _render_tile_over_kernel (Triton)  modules/render.py:121-200
+//   epilogue    canvas fill / clamp / L2 fitness   modules/render.py:235-252, fitness.py:16-31
+//
+// Three launches per batch (fitness) — prep, raster, finalize; two for render.
+//   prep     1 thread / splat: encode (fitness) + preprocess -> 64-B SplatRec in HBM.
+//            Bounds-critical math is ggs_detmath.h (bit-exact with oracle/).
+//   raster   1 workgroup (4 wave64) / (candidate, 64x64 tile).  Order-preserving
+//            cull of the candidate's N splats against the tile (wave ballot +
+//            mbcnt compaction, no global sort) into an LDS list, then a front-to-
+//            back per-pixel blend: wave w owns a 16-column x 64-row strip; lane
+//            (c, r) owns column c and rows r, r+4, ..., r+60 (16 pixels held in
+//            registers).  Per splat the x-dependent half of the Gaussian exponent
+//            is formed once per lane; row groups outside the splat's AABB are
+//            skipped wave-uniformly (scalar branches on readfirstlane'd bounds).
+//            Epilogue: background + clamp, then either the image store (render)
+//            or the weighted squared error summed per tile (fitness; the image
+//            never touches HBM).
+//   finalize 1 workgroup / candidate: fixed-order float64 sum of the tile
+//            partials -> the fitness scalar (deterministic, no atomics).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ggs_detmath.h"
+#include "ggs_internal.h"
+
+namespace ggs {
+
+using namespace detmath;
+
+// ---------------------------------------------------------------------------
+// prep
+// ---------------------------------------------------------------------------
+struct Prep13 {
+    float cx, cy, sxx, sxy, syy, rc, gc, bc, a;
+    int x0, x1, y0, y1;
+};
+
+// encode.py:4-24 + 27-59: axes-angle row -> renderer row (g2, g3, g4 replaced,
+// colours/alpha clamped).  Same op order as oracle/ggs_oracle.py.
+__device__ __forceinline__ void encode_row(const float* __restrict__ g, float out[9]) {
+    const float sx = det_expf(g[2]);
+    const float sy = det_expf(g[3]);
+    float s, c;
+    det_sincosf(g[4], &s, &c);
+    const float sx2 = sx * sx, sy2 = sy * sy, c2 = c * c, s2 = s * s;
+    const float sxx = sx2 * c2 + sy2 * s2;
+    const float sxy = ((sx2 - sy2) * s) * c;
+    const float syy = sx2 * s2 + sy2 * c2;
+    const float l11 = __fsqrt_rn(nmax(sxx, EPS12));
+    const float l21 = __fdiv_rn(sxy, l11);
+    const float l22 = __fsqrt_rn(nmax(syy - l21 * l21, EPS12));
+    out[0] = g[0];
+    out[1] = g[1];
+    out[2] = det_logf(l11);
+    out[3] = det_logf(l22);
+    out[4] = l21;
+#pragma unroll
+    for (int j = 5; j < 9; ++j) out[j] = nclamp(g[j], 0.0f, 255.0f);
+}
+
+// render.py:8-47 on one renderer row.
+__device__ __forceinline__ Prep13 preprocess_row(const float g[9], int H, int W, float k) {
+    Prep13 p;
+    const float maxx = (float)(W - 1), maxy = (float)(H - 1);
+    p.cx = nclamp(g[0], 0.0f, 1.0f) * maxx;
+    p.cy = nclamp(g[1], 0.0f, 1.0f) * maxy;
+    const float l11 = nmax(det_expf(g[2]), EPS6);
+    const float l22 = nmax(det_expf(g[3]), EPS6);
+    const float l21 = g[4];
+    const float hx = nmax(k * fabsf(l11), 1.0f);
+    const float hy = nmax(k * (fabsf(l21) + fabsf(l22)), 1.0f);
+    p.x0 = (int)floorf(nclamp(p.cx - hx, 0.0f, maxx));
+    p.x1 = (int)ceilf(nclamp(p.cx + hx, 0.0f, maxx));
+    p.y0 = (int)floorf(nclamp(p.cy - hy, 0.0f, maxy));
+    p.y1 = (int)ceilf(nclamp(p.cy + hy, 0.0f, maxy));
+    const float i11 = __fdiv_rn(1.0f, l11);
+    const float i22 = __fdiv_rn(1.0f, l22);
+    const float i21 = (-l21) * (i11 * i22);
+    p.sxx = i11 * i11 + i21 * i21;
+    p.sxy = i21 * i22;
+    p.syy = i22 * i22;
+    p.rc = __fdiv_rn(nclamp(g[5], 0.0f, 255.0f), 255.0f);
+    p.gc = __fdiv_rn(nclamp(g[6], 0.0f, 255.0f), 255.0f);
+    p.bc = __fdiv_rn(nclamp(g[7], 0.0f, 255.0f), 255.0f);
+    p.a = __fdiv_rn(nclamp(g[8], 0.0f, 255.0f), 255.0f);
+    return p;
+}
+
+// Raster coefficients.  exp(-0.5*quad)*a == exp2(e) with
+// e = K*(sxx qx^2 + 2 sxy qx qy + syy qy^2) + log2(a),  K = -0.5*log2(e).
+__device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
+    constexpr float K = -0.72134752044448170f;
+    SplatRec r;
+    r.cx = p.cx;
+    r.cy = p.cy;
+    r.A = K * p.sxx;
+    r.Bc = 2.0f * K * p.sxy;
+    r.Cc = K * p.syy;
+    r.la = p.a > 0.0f ? __builtin_amdgcn_logf(p.a) : -__builtin_inff();
+    r.r = p.rc;
+    r.g = p.gc;
+    r.b = p.bc;
+    r.pad0 = r.pad1 = r.pad2 = 0.0f;
+    r.x0 = p.x0;
+    r.x1 = p.x1;
+    r.y0 = p.y0;
+    r.y1 = p.y1;
+    return r;
+}
+
+template <bool ENCODE>
+__global__ void __launch_bounds__(256)
+prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, float k,
+            SplatRec* __restrict__ recs, float* __restrict__ f9, int* __restrict__ i4,
+            float* __restrict__ enc9) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S) return;
+    const float* g = genomes + i * (int64_t)C;
+    float row[9];
+    if (ENCODE) {
+        encode_row(g, row);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 9; ++j) row[j] = g[j];
+    }
+    if (enc9) {
+#pragma unroll
+        for (int j = 0; j < 9; ++j) enc9[i * 9 + j] = row[j];
+    }
+    const Prep13 p = preprocess_row(row, H, W, k);
+    if (recs) recs[i] = make_rec(p);
+    if (f9) {
+        f9[0 * S + i] = p.cx;  f9[1 * S + i] = p.cy;  f9[2 * S + i] = p.sxx;
+        f9[3 * S + i] = p.sxy; f9[4 * S + i] = p.syy; f9[5 * S + i] = p.rc;
+        f9[6 * S + i] = p.gc;  f9[7 * S + i] = p.bc;  f9[8 * S + i] = p.a;
+    }
+    if (i4) {
+        i4[0 * S + i] = p.x0; i4[1 * S + i] = p.x1; i4[2 * S + i] = p.y0; i4[3 * S + i] = p.y1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// raster
+// ---------------------------------------------------------------------------
+constexpr int TILE = 64;          // tile edge (pixels); 4 strips of 16 columns
+constexpr int RG = TILE / 4;      // row groups per lane (rows r, r+4, ...)
+constexpr int NT = 256;           // threads per workgroup
+constexpr int CAP = 512;          // LDS list capacity (records, 32 KiB)
+
+__device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float ufirst(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+// MODE: 0 = write image, 1 = fitness/none, 2 = fitness/weighted, 3 = fitness/boost
+template <int MODE>
+__global__ void __launch_bounds__(NT)
+raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
+              float bg_r, float bg_g, float bg_b, float* __restrict__ img,
+              const float* __restrict__ target, const float* __restrict__ mask, float beta,
+              float* __restrict__ partials, float* __restrict__ wpartials) {
+    __shared__ SplatRec list[CAP];
+    __shared__ int wcnt[4];
+    __shared__ float red[8];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = tid >> 6;
+    const int blk = blockIdx.x;
+    const int b = blk % B;            // tile-major grid: consecutive blocks share a tile
+    const int t = blk / B;
+    const int tx0 = (t % nTX) * TILE;
+    const int ty0 = (t / nTX) * TILE;
+    const int tx1 = min(tx0 + TILE, W) - 1;
+    const int ty1 = min(ty0 + TILE, H) - 1;
+
+    const int sx0 = tx0 + wv * 16;    // this wave's strip: columns [sx0, sx0+15]
+    const int col = sx0 + (lane & 15);
+    const int ph = lane >> 4;         // row phase 0..3
+    const float Xf = (float)col;
+    const float Yb = (float)(ty0 + ph);
+
+    float R[RG], G[RG], Bl[RG], T[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) { R[g] = 0.0f; G[g] = 0.0f; Bl[g] = 0.0f; T[g] = 1.0f; }
+
+    const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int cnt = 0;
+
+    for (int base = 0; base < N; base += NT) {
+        // --- cull: splats in DESCENDING index order (front-to-back) ----------
+        const int i = N - 1 - (base + tid);
+        bool hit = false;
+        if (i >= 0) {
+            const int4 bb = *reinterpret_cast<const int4*>(&crec[i].x0);
+            hit = !(bb.y < tx0 || bb.x > tx1 || bb.w < ty0 || bb.z > ty1);
+        }
+        const uint64_t m = __ballot(hit);
+        if (lane == 0) wcnt[wv] = __popcll(m);
+        __syncthreads();
+        int off = cnt;
+        for (int w = 0; w < wv; ++w) off += wcnt[w];
+        const int total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        if (hit) list[off + __popcll(m & lt_mask)] = crec[i];
+        cnt += total;
+        __syncthreads();
+        if (cnt <= CAP - NT && base + NT < N) continue;
+
+        // --- blend the list ------------------------------------------------
+        for (int j = 0; j < cnt; ++j) {
+            const SplatRec s = list[j];
+            const int x0 = ufirst(s.x0), x1 = ufirst(s.x1);
+            if (x1 < sx0 || x0 > sx0 + 15) continue;          // strip miss (uniform)
+            const int y0 = ufirst(s.y0), y1 = ufirst(s.y1);
+            const int gA = max(y0 - ty0, 0) >> 2;
+            const int gB = min((y1 - ty0) >> 2, RG - 1);
+            const bool partA = (ty0 + 4 * gA) < y0;
+            const bool partB = (ty0 + 4 * gB + 3) > y1;
+            const float cx = ufirst(s.cx), cy = ufirst(s.cy);
+            const float A = ufirst(s.A), Bc = ufirst(s.Bc), Cc = ufirst(s.Cc), la = ufirst(s.la);
+            const float cr = ufirst(s.r), cg = ufirst(s.g), cb = ufirst(s.b);
+
+            const float qx = Xf - cx;
+            const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
+            const float px = inx ? __builtin_fmaf(A * qx, qx, la) : -__builtin_inff();
+            const float bx = Bc * qx;
+            const float qy0 = Yb - cy;
+#pragma unroll
+            for (int g = 0; g < RG; ++g) {
+                if (g < gA || g > gB) continue;
+                const float qy = qy0 + (float)(4 * g);
+                float e = __builtin_fmaf(qy, __builtin_fmaf(Cc, qy, bx), px);
+                if ((g == gA && partA) || (g == gB && partB)) {
+                    const int row = ty0 + 4 * g + ph;
+                    if ((unsigned)(row - y0) > (unsigned)(y1 - y0)) e = -__builtin_inff();
+                }
+                const float f = __builtin_amdgcn_exp2f(e);
+                const float w = T[g] * f;
+                R[g] = __builtin_fmaf(w, cr, R[g]);
+                G[g] = __builtin_fmaf(w, cg, G[g]);
+                Bl[g] = __builtin_fmaf(w, cb, Bl[g]);
+                T[g] = T[g] - w;
+            }
+        }
+        cnt = 0;
+        __syncthreads();   // list is rewritten by the next cull round
+    }
+
+    // --- epilogue ---------------------------------------------------------------
+    if (MODE == 0) {
+        if (col < W) {
+#pragma unroll
+            for (int g = 0; g < RG; ++g) {
+                const int row = ty0 + 4 * g + ph;
+                if (row < H) {
+                    float* o = img + (((int64_t)b * H + row) * W + col) * 3;
+                    o[0] = fminf(fmaxf(__builtin_fmaf(T[g], bg_r, R[g]), 0.0f), 1.0f);
+                    o[1] = fminf(fmaxf(__builtin_fmaf(T[g], bg_g, G[g]), 0.0f), 1.0f);
+                    o[2] = fminf(fmaxf(__builtin_fmaf(T[g], bg_b, Bl[g]), 0.0f), 1.0f);
+                }
+            }
+        }
+        return;
+    } else {
+        float acc = 0.0f, wacc = 0.0f;
+        if (col < W) {
+#pragma unroll
+            for (int g = 0; g < RG; ++g) {
+                const int row = ty0 + 4 * g + ph;
+                if (row < H) {
+                    const int64_t p = (int64_t)row * W + col;
+                    const float cr = fminf(fmaxf(__builtin_fmaf(T[g], bg_r, R[g]), 0.0f), 1.0f);
+                    const float cg = fminf(fmaxf(__builtin_fmaf(T[g], bg_g, G[g]), 0.0f), 1.0f);
+                    const float cb = fminf(fmaxf(__builtin_fmaf(T[g], bg_b, Bl[g]), 0.0f), 1.0f);
+                    const float dr = cr - target[p * 3 + 0];
+                    const float dg = cg - target[p * 3 + 1];
+                    const float db = cb - target[p * 3 + 2];
+                    const float d2 = dr * dr + dg * dg + db * db;
+                    float wgt = 1.0f;
+                    if (MODE == 2) wgt = mask[p];
+                    if (MODE == 3) wgt = 1.0f + beta * fminf(fmaxf(mask[p], 0.0f), 1.0f);
+                    acc += wgt * d2;
+                    wacc += wgt;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            acc += __shfl_xor(acc, o);
+            wacc += __shfl_xor(wacc, o);
+        }
+        if (lane == 0) { red[wv] = acc; red[4 + wv] = wacc; }
+        __syncthreads();
+        if (tid == 0) {
+            partials[(int64_t)b * nTiles + t] = (red[0] + red[1]) + (red[2] + red[3]);
+            if (b == 0 && wpartials) wpartials[t] = (red[4] + red[5]) + (red[6] + red[7]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// finalize: fixed-order float64 reduction of tile partials -> fitness scalar
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+finalize_kernel(const float* __restrict__ partials, const float* __restrict__ wpartials,
+                int nTiles, int mode, double hw, float* __restrict__ out) {
+    __shared__ double sd[256];
+    __shared__ double sw[256];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    double s = 0.0, w = 0.0;
+    for (int i = tid; i < nTiles; i += 256) {
+        s += (double)partials[(int64_t)b * nTiles + i];
+        if (mode != GGS_FIT_NONE) w += (double)wpartials[i];
+    }
+    sd[tid] = s;
+    sw[tid] = w;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) { sd[tid] += sd[tid + o]; sw[tid] += sw[tid + o]; }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const double num = sd[0], wsum = sw[0];
+        double v;
+        if (mode == GGS_FIT_NONE) v = num / (3.0 * hw);                       // fitness.py:18-19
+        else if (mode == GGS_FIT_WEIGHTED) v = num / (wsum + 1e-12);          // fitness.py:28-31
+        else v = (num / (3.0 * hw)) / (wsum / hw + 1e-12);                    // fitness.py:23-27
+        out[b] = (float)v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers (called from ggs_capi.cpp; no allocation, no sync)
+// ---------------------------------------------------------------------------
+hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_t S, int C, int H,
+                       int W, float k, SplatRec* recs, float* f9, int* i4, float* enc9) {
+    if (S <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)((S + 255) / 256);
+    if (encode)
+        hipLaunchKernelGGL(prep_kernel<true>, dim3(grid), dim3(256), 0, st, genomes, S, C, H, W, k,
+                           recs, f9, i4, enc9);
+    else
+        hipLaunchKernelGGL(prep_kernel<false>, dim3(grid), dim3(256), 0, st, genomes, S, C, H, W, k,
+                           recs, f9, i4, enc9);
+    return hipGetLastError();
+}
+
+int raster_tiles(int H, int W, int* nTX) {
+    const int tx = (W + TILE - 1) / TILE, ty = (H + TILE - 1) / TILE;
+    if (nTX) *nTX = tx;
+    return tx * ty;
+}
+
+hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
+                         const float bg[3], float* img, const float* target, const float* mask,
+                         float beta, float* partials, float* wpartials) {
+    int nTX;
+    const int nTiles = raster_tiles(H, W, &nTX);
+    const dim3 grid((unsigned)((int64_t)B * nTiles)), block(NT);
+#define GGS_RASTER(M)                                                                          \
+    hipLaunchKernelGGL(raster_kernel<M>, grid, block, 0, st, recs, B, N, H, W, nTX, nTiles,     \
+                       bg[0], bg[1], bg[2], img, target, mask, beta, partials, wpartials)
+    switch (mode) {
+        case 0: GGS_RASTER(0); break;
+        case 1: GGS_RASTER(1); break;
+        case 2: GGS_RASTER(2); break;
+        default: GGS_RASTER(3); break;
+    }
+#undef GGS_RASTER
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,
+                           int nTiles, int mode, int H, int W, float* out) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(B), dim3(256), 0, st, partials, wpartials, nTiles, mode,
+                       (double)H * (double)W, out);
+    return hipGetLastError();
+}
+
+}  // namespace ggs

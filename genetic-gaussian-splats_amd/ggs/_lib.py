@@ -1,0 +1,114 @@
+"""ctypes binding of libggs.so (C ABI declared in include/ggs.h).
+
+The product path is this library and nothing else: if libggs.so is missing or
+cannot be loaded, importing ``ggs`` raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("GGS_LIB", os.path.join(_PKG_ROOT, "libggs.so"))
+
+GGS_OK, GGS_EINVAL, GGS_ENODEV, GGS_EHIP, GGS_ENOMEM = 0, -1, -2, -3, -4
+GGS_FIT_NONE, GGS_FIT_WEIGHTED, GGS_FIT_BOOST = 0, 1, 2
+
+_f32p = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int32)
+
+# name -> (restype, argtypes); mirrors include/ggs.h one-for-one
+SIGNATURES = {
+    "ggs_version": (C.c_char_p, []),
+    "ggs_init": (C.c_int, [C.c_int32]),
+    "ggs_device_count": (C.c_int, []),
+    "ggs_select_devices": (C.c_int, [_i32p, C.c_int32]),
+    "ggs_last_error": (C.c_char_p, []),
+    "ggs_shutdown": (None, []),
+    "ggs_render": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                             C.c_float, _f32p, _f32p, C.c_int32]),
+    "ggs_fitness": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int32,
+                              C.c_float, C.c_int32, C.c_int32, C.c_float, _f32p, C.c_int32]),
+    "ggs_encode": (C.c_int, [_f32p, C.c_int64, C.c_int32, _f32p]),
+    "ggs_preprocess": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_float,
+                                 _f32p, _i32p]),
+    "ggs_render_device": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32,
+                                    C.c_int32, C.c_int32, C.c_int32, C.c_float, _f32p, C.c_void_p]),
+    "ggs_fitness_device": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32,
+                                     C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_float,
+                                     C.c_int32, C.c_int32, C.c_float, C.c_void_p]),
+    "ggs_profile_enable": (C.c_int, [C.c_int32]),
+    "ggs_profile_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "ggs_profile_reset": (None, []),
+}
+
+
+class GGSError(RuntimeError):
+    """A libggs call failed (HIP runtime error, allocation failure, ...)."""
+
+
+class GGSDeviceError(GGSError, AssertionError):
+    """No usable HIP device — the reference's ``assert dev.type == "cuda"``
+    (render.py:217) raises AssertionError; this subclasses it as well."""
+
+
+class GGSInputError(AssertionError, ValueError):
+    """Bad argument.  The reference reports these through ``assert``
+    (render.py:219, :223), hence the AssertionError base; ValueError too."""
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libggs.so not found at {LIB_PATH}: build it with "
+            f"`make -C {os.path.join(_PKG_ROOT, 'csrc')}` (or __graft_entry__.build()). "
+            "There is no CPU fallback.")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+_init_lock = threading.Lock()
+
+
+def last_error() -> str:
+    msg = lib.ggs_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc == GGS_OK:
+        return
+    msg = f"{what}: {last_error()}"
+    if rc == GGS_EINVAL:
+        raise GGSInputError(msg)
+    if rc == GGS_ENODEV:
+        raise GGSDeviceError(msg)
+    raise GGSError(f"{msg} (code {rc})")
+
+
+def select_devices(ids) -> int:
+    """Restrict the host API to these HIP device ids (empty: all)."""
+    ensure_init()
+    arr = (C.c_int32 * max(len(ids), 1))(*ids)
+    rc = lib.ggs_select_devices(arr, len(ids))
+    if rc < 0:
+        check(rc, "ggs_select_devices")
+    return rc
+
+
+def ensure_init() -> int:
+    """Initialise every visible HIP device once; returns the device count."""
+    with _init_lock:
+        n = lib.ggs_device_count()
+        if n > 0:
+            return n
+        rc = lib.ggs_init(0)
+        if rc < 0:
+            check(rc, "ggs_init")
+        return rc

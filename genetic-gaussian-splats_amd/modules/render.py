@@ -1,0 +1,25 @@
+"""Drop-in for the reference's modules/render.py (render.py:1-252).
+
+``render_splats_rgb_triton`` keeps the reference signature; the work runs in
+libggs.so (HIP, gfx950): prep + order-preserving per-tile cull + front-to-back
+blend, one launch each.  ``tile``, ``num_warps`` and ``num_stages`` are accepted
+and ignored — the reference output is tile-invariant and the
+MI355X kernel picks its own tiling.  ``use_fp16_canvas`` (never used by any
+reference caller) is accepted; the canvas is always float32.
+"""
+from __future__ import annotations
+
+from modules._compat import check_device, ggs, like
+
+_DEV = "cuda"   # imported by run_ggs.py:8 / run_sags.py:8; 'cuda' is ROCm's HIP device type
+__all__ = ["render_splats_rgb_triton", "_DEV"]
+
+
+def render_splats_rgb_triton(genomes, H: int, W: int, *, k_sigma: float = 3.0, device=None,
+                             background=(1.0, 1.0, 1.0), tile: int = 64, num_warps: int = 8,
+                             num_stages: int = 3, use_fp16_canvas: bool = False):
+    """render.py:203-252 → [B,H,W,3] float32 clamped to [0,1] (numpy, or torch
+    on the input's device when given a torch tensor)."""
+    check_device(device or _DEV)
+    out = ggs.render(genomes, H, W, k_sigma=k_sigma, background=background)
+    return like(out, genomes)

@@ -1,0 +1,124 @@
+/*
+ * ggs.h — C ABI of libggs.so, the MI355X (gfx950) 2D Gaussian-splat renderer and
+ * fitness evaluator.  Plain pointers and sizes only; no torch/HIP types in any
+ * signature (device streams are passed as void*).
+ *
+ * It is the drop-in boundary for the reference's hot path
+ * (josedelrey/genetic-gaussian-splats):
+ *
+ *   ggs_render          <- modules/render.py:203-252  render_splats_rgb_triton
+ *                          (with render.py:8-47 _preprocess_genome,
+ *                           render.py:50-118 _gpu_bin_splats_to_tiles,
+ *                           render.py:121-200 _render_tile_over_kernel)
+ *   ggs_fitness         <- modules/fitness.py:7-31  fitness_many
+ *                          (with modules/encode.py:62-79 genome_to_renderer_batched;
+ *                           fitness.py:34-47 fitness_population is a host-side loop)
+ *   ggs_encode          <- modules/encode.py:27-79  genome_to_renderer(_batched)
+ *   ggs_preprocess      <- modules/render.py:8-47   _preprocess_genome
+ *   ggs_*_device        the same two operations on caller-owned device memory
+ *                        (inputs already resident in HBM, caller's HIP stream)
+ *
+ * Genome layouts (row-major float32, C >= 9 columns per splat, extra columns
+ * ignored as render.py:222-223 does):
+ *   axes-angle (fitness input, population.py:43):  x, y, a_log, b_log, theta, r, g, b, alpha
+ *   renderer   (render input,  encode.py:37-57):   x, y, log l11, log l22, l21, r, g, b, alpha
+ *
+ * Ownership: all pointers are caller-owned and only used during the call (host
+ * API: the call is synchronous; device API: the work is enqueued on `stream`
+ * and the pointers must stay valid until it completes).  The library keeps
+ * pooled device workspaces and a cache of the last target/mask uploaded per
+ * device (keyed by size + a 64-bit content hash).
+ *
+ * Errors: 0 on success, a negative GGS_E* code otherwise; ggs_last_error()
+ * returns a thread-local message.  The reference's assertion failures
+ * (render.py:217 CUDA device, :219 ndim, :223 C >= 9) map to GGS_ENODEV and
+ * GGS_EINVAL.  Thread safety: calls may come from any thread; each device
+ * context is guarded by its own mutex.
+ */
+#ifndef GGS_H_
+#define GGS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GGS_OK 0
+#define GGS_EINVAL (-1) /* bad argument (reference asserts render.py:219,223) */
+#define GGS_ENODEV (-2) /* no usable HIP device (reference assert render.py:217) */
+#define GGS_EHIP (-3)   /* HIP runtime / launch failure */
+#define GGS_ENOMEM (-4) /* device or pinned host allocation failed */
+
+/* fitness modes (fitness.py:17-31) */
+#define GGS_FIT_NONE 0     /* weight_mask is None:  mean over H*W*3 of d^2          */
+#define GGS_FIT_WEIGHTED 1 /* default GA path:      sum(w*d^2) / (sum(w) + 1e-12)   */
+#define GGS_FIT_BOOST 2    /* boost_only=True:      mean(d^2*wb) / (mean(wb)+1e-12), wb = 1+beta*clamp(w,0,1) */
+
+/* Library version string. */
+const char* ggs_version(void);
+
+/* Initialise up to max_devices HIP devices (<=0: all).  Returns the number of
+ * usable devices (>0) or a negative error.  Idempotent; called lazily by every
+ * entry point. */
+int ggs_init(int32_t max_devices);
+
+/* Number of HIP devices the library sees (0 before ggs_init / without GPUs). */
+int ggs_device_count(void);
+
+/* Restrict the host API's fan-out to the listed device ids, in order (n == 0:
+ * all devices).  One process per GPU calls this with its local rank.  Device
+ * contexts are created lazily on first use.  Returns the active count. */
+int ggs_select_devices(const int32_t* ids, int32_t n);
+
+/* Thread-local message describing the last error on this thread ("" if none). */
+const char* ggs_last_error(void);
+
+/* Free every device buffer, stream and pinned host buffer. */
+void ggs_shutdown(void);
+
+/* ---- host-pointer API (drop-in path) ----------------------------------------
+ * render: genomes [B,N,C] renderer layout -> out [B,H,W,3] in [0,1].
+ *   bg: background RGB (render.py:209, default 1,1,1); NULL means (1,1,1).
+ * fitness: genomes [B,N,C] axes-angle layout, target [H,W,3], mask [H,W]
+ *   (NULL iff mode == GGS_FIT_NONE) -> out [B] float32.
+ * n_devices: shard the B candidates contiguously over the first n_devices of
+ *   the active device list (<=0: all of them; see ggs_select_devices). */
+int ggs_render(const float* genomes, int64_t B, int32_t N, int32_t C, int32_t H, int32_t W,
+               float k_sigma, const float* bg, float* out_bhw3, int32_t n_devices);
+int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, const float* target_hw3,
+                const float* mask_hw, int32_t mode, float boost_beta, int32_t H, int32_t W,
+                float k_sigma, float* out_B, int32_t n_devices);
+
+/* ---- stage exports (host pointers; parity tests) ----------------------------
+ * encode: S splat rows (stride C) axes-angle -> renderer rows [S,9].
+ * preprocess: S renderer rows (stride C) -> out_f9 [9][S] = cx, cy, sxx, sxy,
+ *   syy, rc, gc, bc, a and out_i4 [4][S] = x0, x1, y0, y1 (render.py:45-47). */
+int ggs_encode(const float* genomes_axes, int64_t S, int32_t C, float* out_S9);
+int ggs_preprocess(const float* genomes, int64_t S, int32_t C, int32_t H, int32_t W, float k_sigma,
+                   float* out_f9, int32_t* out_i4);
+
+/* ---- device-pointer API (inputs resident in HBM) ----------------------------
+ * Same semantics as the host API on one device; all pointers are device
+ * pointers on `device`; work is enqueued on `stream` (a hipStream_t, NULL =
+ * the null stream) and the call returns without synchronising. */
+int ggs_render_device(int32_t device, void* stream, const float* d_genomes, int64_t B, int32_t N,
+                      int32_t C, int32_t H, int32_t W, float k_sigma, const float* bg,
+                      float* d_out_bhw3);
+int ggs_fitness_device(int32_t device, void* stream, const float* d_genomes_axes, int64_t B,
+                       int32_t N, int32_t C, const float* d_target_hw3, const float* d_mask_hw,
+                       int32_t mode, float boost_beta, int32_t H, int32_t W, float k_sigma,
+                       float* d_out_B);
+
+/* ---- per-kernel timing (HIP events on the launch stream) --------------------
+ * When enabled, every launch of "prep", "raster" and "finalize" is bracketed
+ * by hipEvents; ggs_profile_read synchronises those events and returns the
+ * accumulated milliseconds and launch count for the named kernel. */
+int ggs_profile_enable(int32_t on);
+int ggs_profile_read(const char* kernel, double* total_ms, int64_t* launches);
+void ggs_profile_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GGS_H_ */

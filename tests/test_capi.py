@@ -1,0 +1,122 @@
+"""The C-ABI boundary on CPU: libggs.so loads, exports exactly what
+include/ggs.h declares, the ctypes table matches, and argument validation (the
+reference's assert conditions) happens before any device work.  No compute."""
+from __future__ import annotations
+
+import inspect
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG, REPO
+
+HEADER = os.path.join(REPO, "include", "ggs.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ggs_\w+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("ggs_render", "ggs_fitness", "ggs_render_device", "ggs_fitness_device",
+                 "ggs_encode", "ggs_preprocess", "ggs_last_error", "ggs_init"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    import ggs
+    names = declared_functions()
+    out = subprocess.run(["nm", "-D", "--defined-only", ggs.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\sT\s+(ggs_\w+)$", out, flags=re.M))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    for n in names:
+        assert hasattr(ggs.lib, n)
+
+
+def test_ctypes_table_matches_header():
+    from ggs import _lib
+    assert sorted(_lib.SIGNATURES) == declared_functions()
+
+
+def test_version_and_error_string():
+    import ggs
+    assert b"gfx950" in ggs.lib.ggs_version()
+    assert isinstance(ggs.lib.ggs_last_error(), bytes)
+
+
+def test_input_validation_mirrors_reference_asserts():
+    import ggs
+    tgt = np.zeros((8, 8, 3), np.float32)
+    with pytest.raises(AssertionError):                      # render.py:223
+        ggs.fitness(np.zeros((2, 3, 8), np.float32), tgt, 8, 8)
+    with pytest.raises(ValueError):                          # render.py:219
+        ggs.render(np.zeros((2, 2, 3, 9), np.float32), 8, 8)
+    with pytest.raises(ggs.GGSInputError):
+        ggs.fitness(np.zeros((2, 3, 9), np.float32), tgt, 8, 9)   # target shape
+    # the C layer validates too (before touching a device)
+    import ctypes as C
+    rc = ggs.lib.ggs_render(None, 1, 1, 8, 4, 4, 3.0, None, None, 0)
+    assert rc == -1 and b"9 genome cols" in ggs.lib.ggs_last_error()
+    rc = ggs.lib.ggs_fitness(None, 1, 1, 9, None, None, 7, 1.0, 4, 4, 3.0, None, 0)
+    assert rc == -1
+    rc = ggs.lib.ggs_fitness_device(0, None, None, 1, 1, 9, None, None, 1, 1.0, 4, 4, 3.0, None)
+    assert rc == -1 and b"mask" in ggs.lib.ggs_last_error()
+    del C
+
+
+def test_no_device_is_an_assertion_like_the_reference():
+    import ggs
+    if ggs.lib.ggs_init(0) > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(AssertionError):                      # render.py:217
+        ggs.render(np.zeros((1, 1, 9), np.float32), 4, 4)
+
+
+# reference signatures (modules/render.py:204-214, fitness.py:8-12, fitness.py:35-39,
+# encode.py:4, :28, :63) — the drop-ins must accept the same parameters
+REF_SIGS = {
+    ("render", "render_splats_rgb_triton"):
+        ["genomes", "H", "W", "*k_sigma=3.0", "*device=None", "*background=(1.0, 1.0, 1.0)",
+         "*tile=64", "*num_warps=8", "*num_stages=3", "*use_fp16_canvas=False"],
+    ("fitness", "fitness_many"):
+        ["pop_batch", "target", "H", "W", "k_sigma", "device", "tile=32", "weight_mask=None",
+         "boost_only=False", "boost_beta=1.0"],
+    ("fitness", "fitness_population"):
+        ["population", "target", "H", "W", "k_sigma", "device", "tile=32", "chunk=None",
+         "weight_mask=None", "boost_only=False"],
+    ("encode", "axes_angle_to_cholesky"): ["a_log", "b_log", "theta"],
+    ("encode", "genome_to_renderer"): ["ind_axes_angle"],
+    ("encode", "genome_to_renderer_batched"): ["G_axes"],
+}
+
+
+@pytest.mark.parametrize("mod,fn", sorted(REF_SIGS))
+def test_drop_in_signatures_match_reference(mod, fn):
+    import importlib
+    m = importlib.import_module(f"modules.{mod}")
+    sig = inspect.signature(getattr(m, fn))
+    got = []
+    for p in sig.parameters.values():
+        s = ("*" if p.kind == p.KEYWORD_ONLY else "") + p.name
+        if p.default is not p.empty:
+            s += f"={p.default!r}"
+        got.append(s)
+    assert got == REF_SIGS[(mod, fn)]
+
+
+def test_drop_in_keeps_module_constant():
+    from modules import render
+    assert render._DEV == "cuda" and "render_splats_rgb_triton" in render.__all__
+
+
+def test_package_layout():
+    assert os.path.isfile(os.path.join(PKG, "libggs.so"))
+    assert os.path.isdir(os.path.join(PKG, "csrc"))

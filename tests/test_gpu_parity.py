@@ -1,0 +1,248 @@
+"""Parity of the HIP path (libggs.so via its C ABI) with the oracle and with the
+reference's golden vectors.  Needs an MI355X: run with ``-m gpu``.
+
+Bars (north_star / SURVEY.md §8c):
+* encode + preprocess: BIT-EXACT against the oracle (integer bounds and floats) —
+  both sides use the deterministic float32 functions of oracle/detmath.py;
+* rendered images: ≤ 1e-4 abs against the reference golden images and the oracle;
+* fitness scalars: rel ≤ 1e-5 against the reference golden values and the oracle;
+* full-size (512²/256/B=128) through size-independent properties: fused fitness
+  == fitness of the rendered images, bit-reproducible reruns, shard invariance.
+"""
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import ggs
+import ggs_oracle as O
+from conftest import GOLDEN, load_golden
+
+pytestmark = pytest.mark.gpu
+IMG_TOL = 1e-4
+FIT_RTOL = 1e-5
+
+
+def _render_cases():
+    return sorted(os.path.basename(p)[7:-4] for p in glob.glob(os.path.join(GOLDEN, "render_*.npz")))
+
+
+def test_device_present_and_library_native():
+    n = ggs.ensure_init()
+    assert n >= 1
+    # the product path is libggs.so, loaded in-tree
+    maps = open("/proc/self/maps").read()
+    assert ggs.LIB_PATH in maps
+
+
+# ---- stage parity: bit-exact with the oracle ---------------------------------------
+@pytest.mark.parametrize("case", ["edge", "syn"])
+def test_encode_bit_exact_vs_oracle(case):
+    G = load_golden("encode.npz")[f"{case}_in"]
+    np.testing.assert_array_equal(ggs.encode(G), O.genome_to_renderer_batched(G))
+
+
+def test_encode_bit_exact_random_large():
+    rng = np.random.default_rng(0)
+    G = O.synthetic_population(8, 1024, 1024, 1024, seed=3)
+    G[..., 4] = rng.uniform(-50, 50, G.shape[:2])          # unwrapped angles too
+    np.testing.assert_array_equal(ggs.encode(G), O.genome_to_renderer_batched(G))
+
+
+def _assert_prep_equal(got, ref):
+    for k in O.BOUND_KEYS + O.FLOAT_KEYS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize("case", ["edge", "syn512", "raw", "k2", "w1"])
+def test_preprocess_bit_exact_vs_oracle(case):
+    d = load_golden("preprocess.npz")
+    H, W, k = d[f"{case}__HWk"]
+    g = d[f"{case}__in"]
+    _assert_prep_equal(ggs.preprocess(g, int(H), int(W), float(k)),
+                       O.preprocess(g, int(H), int(W), float(k)))
+
+
+def test_preprocess_of_encoded_population_bit_exact_large():
+    """The fitness path's bounds: encode -> preprocess at 1024^2, 32k splats."""
+    G = O.synthetic_population(32, 1024, 1024, 1024, seed=9)
+    enc = ggs.encode(G).reshape(-1, 9)
+    _assert_prep_equal(ggs.preprocess(enc, 1024, 1024, 3.0), O.preprocess(enc, 1024, 1024, 3.0))
+
+
+# ---- render parity ---------------------------------------------------------------------
+@pytest.mark.parametrize("case", _render_cases())
+def test_render_matches_reference_golden(case):
+    d = load_golden(f"render_{case}.npz")
+    H, W, k = d["HWk"]
+    out = ggs.render(d["genomes"], int(H), int(W), k_sigma=float(k), background=tuple(d["bg"]))
+    for key in (key for key in d.files if key.startswith("img_t")):
+        np.testing.assert_allclose(out, d[key].reshape(out.shape), atol=IMG_TOL, rtol=0,
+                                   err_msg=key)
+    ref = O.render(d["genomes"], int(H), int(W), k_sigma=float(k), background=tuple(d["bg"]))
+    np.testing.assert_allclose(out, ref, atol=IMG_TOL, rtol=0)
+
+
+@pytest.mark.parametrize("H,W,N,B,seed", [(256, 256, 64, 2, 1), (512, 512, 256, 1, 2),
+                                          (200, 333, 100, 3, 3), (1, 1, 5, 2, 4),
+                                          (1, 130, 20, 1, 5), (97, 1, 20, 1, 6)])
+def test_render_vs_oracle_sizes(H, W, N, B, seed):
+    G9 = O.genome_to_renderer_batched(O.synthetic_population(B, N, H, W, seed=seed))
+    np.testing.assert_allclose(ggs.render(G9, H, W), O.render(G9, H, W), atol=IMG_TOL, rtol=0)
+
+
+def test_render_list_overflow_many_overlapping_splats():
+    """> LDS list capacity per tile: 1500 large splats all covering every tile."""
+    rng = np.random.default_rng(11)
+    N, H, W = 1500, 96, 80
+    G = np.zeros((1, N, 9), np.float32)
+    G[..., 0:2] = rng.uniform(0.3, 0.7, (1, N, 2))
+    G[..., 2:4] = np.log(rng.uniform(30, 60, (1, N, 2)))
+    G[..., 4] = rng.uniform(-5, 5, (1, N))
+    G[..., 5:8] = rng.uniform(0, 255, (1, N, 3))
+    G[..., 8] = rng.uniform(0, 40, (1, N))
+    np.testing.assert_allclose(ggs.render(G, H, W), O.render(G, H, W), atol=IMG_TOL, rtol=0)
+
+
+def test_render_edge_inputs():
+    H, W = 40, 50
+    assert ggs.render(np.zeros((0, 3, 9), np.float32), H, W).shape == (0, H, W, 3)
+    empty = ggs.render(np.zeros((2, 0, 9), np.float32), H, W, background=(0.2, 1.5, -1.0))
+    np.testing.assert_array_equal(empty, np.broadcast_to(np.float32([0.2, 1.0, 0.0]), empty.shape))
+    g = O.genome_to_renderer_batched(O.synthetic_population(2, 30, H, W, seed=1))
+    g12 = np.concatenate([g, np.full((2, 30, 3), 9.0, np.float32)], -1)
+    np.testing.assert_array_equal(ggs.render(g12, H, W), ggs.render(g, H, W))
+    np.testing.assert_array_equal(ggs.render(g[0], H, W), ggs.render(g[:1], H, W))
+    np.testing.assert_allclose(ggs.render(g, H, W, k_sigma=1.5), O.render(g, H, W, k_sigma=1.5),
+                               atol=IMG_TOL, rtol=0)
+
+
+# ---- fitness parity ------------------------------------------------------------------------
+@pytest.mark.parametrize("case", ["f64", "f128", "f40x56"])
+def test_fitness_matches_reference_golden(case):
+    d = load_golden("fitness.npz")
+    H, W = (int(v) for v in d[f"{case}__HW"])
+    pop, tgt, mask = d[f"{case}__pop"], d[f"{case}__target"], d[f"{case}__mask"]
+    for mode, kw in (("none", {}), ("weighted", {"weight_mask": mask}),
+                     ("boost", {"weight_mask": mask, "boost_only": True})):
+        got = ggs.fitness(pop, tgt, H, W, 3.0, **kw)
+        np.testing.assert_allclose(got, d[f"{case}__{mode}"], rtol=FIT_RTOL, err_msg=mode)
+        np.testing.assert_allclose(got, O.fitness_many(list(pop), tgt, H, W, 3.0, **kw),
+                                   rtol=FIT_RTOL, err_msg=mode)
+    chunked = ggs.fitness_population(list(pop), tgt, H, W, 3.0, chunk=2, weight_mask=mask)
+    np.testing.assert_allclose(chunked, d[f"{case}__pop_chunk2"], rtol=FIT_RTOL)
+
+
+def test_fitness_vs_oracle_512():
+    H = W = 512
+    pop = O.synthetic_population(4, 256, H, W, seed=21)
+    rng = np.random.default_rng(5)
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
+    for kw in ({}, {"weight_mask": mask}, {"weight_mask": mask, "boost_only": True}):
+        np.testing.assert_allclose(ggs.fitness(pop, tgt, H, W, 3.0, **kw),
+                                   O.fitness_many(list(pop), tgt, H, W, 3.0, **kw), rtol=FIT_RTOL)
+
+
+# ---- full-size properties (512^2 / 256 splats / pop 128) -------------------------------------
+@pytest.fixture(scope="module")
+def full_size():
+    H = W = 512
+    pop = O.synthetic_population(128, 256, H, W, seed=0)
+    rng = np.random.default_rng(1)
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
+    return pop, tgt, mask, H, W
+
+
+def test_full_size_fused_fitness_equals_fitness_of_rendered_images(full_size):
+    pop, tgt, mask, H, W = full_size
+    fused = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+    imgs = ggs.render(ggs.encode(pop), H, W)
+    d2 = ((imgs.astype(np.float64) - tgt[None]) ** 2).sum(-1)
+    ref = (d2 * mask[None]).sum((1, 2)) / (mask.astype(np.float64).sum() + 1e-12)
+    np.testing.assert_allclose(fused, ref, rtol=FIT_RTOL)
+
+
+def test_full_size_bit_reproducible_and_shard_invariant(full_size):
+    pop, tgt, mask, H, W = full_size
+    a = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+    b = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+    np.testing.assert_array_equal(a, b)
+    parts = np.concatenate([ggs.fitness(pop[i:i + 37], tgt, H, W, 3.0, weight_mask=mask)
+                            for i in range(0, len(pop), 37)])
+    np.testing.assert_array_equal(a, parts)
+    one = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask, n_devices=1)
+    np.testing.assert_array_equal(a, one)
+
+
+def test_full_size_sample_vs_oracle(full_size):
+    pop, tgt, mask, H, W = full_size
+    idx = [0, 63, 127]
+    got = ggs.fitness(pop[idx], tgt, H, W, 3.0, weight_mask=mask)
+    np.testing.assert_allclose(got, O.fitness_many(list(pop[idx]), tgt, H, W, 3.0, weight_mask=mask),
+                               rtol=FIT_RTOL)
+
+
+def test_target_cache_sees_content_change(full_size):
+    pop, tgt, mask, H, W = full_size
+    a = ggs.fitness(pop[:4], tgt, H, W, 3.0, weight_mask=mask)
+    tgt2 = tgt.copy()
+    tgt2[100:200, 100:200] = 0.0
+    b = ggs.fitness(pop[:4], tgt2, H, W, 3.0, weight_mask=mask)
+    assert (a != b).all()
+    np.testing.assert_array_equal(ggs.fitness(pop[:4], tgt, H, W, 3.0, weight_mask=mask), a)
+
+
+# ---- device-pointer API (inputs resident in HBM) ---------------------------------------------
+def test_device_api_matches_host_api(full_size):
+    torch = pytest.importorskip("torch")
+    pop, tgt, mask, H, W = full_size
+    dev = torch.device("cuda:0")
+    dg = torch.from_numpy(pop[:16]).to(dev)
+    dt = torch.from_numpy(tgt).to(dev)
+    dm = torch.from_numpy(mask).to(dev)
+    out = torch.empty(16, dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for mode, m in ((ggs.GGS_FIT_NONE, 0), (ggs.GGS_FIT_WEIGHTED, dm.data_ptr()),
+                    (ggs.GGS_FIT_BOOST, dm.data_ptr())):
+        ggs.fitness_device(0, st, dg.data_ptr(), 16, 256, 9, dt.data_ptr(), m, mode, 1.0, H, W, 3.0,
+                           out.data_ptr())
+        torch.cuda.synchronize()
+        kw = {} if mode == ggs.GGS_FIT_NONE else {"weight_mask": mask,
+                                                  "boost_only": mode == ggs.GGS_FIT_BOOST}
+        np.testing.assert_array_equal(out.cpu().numpy(), ggs.fitness(pop[:16], tgt, H, W, 3.0, **kw))
+    img = torch.empty((2, H, W, 3), dtype=torch.float32, device=dev)
+    g9 = torch.from_numpy(ggs.encode(pop[:2])).to(dev)
+    ggs.render_device(0, st, g9.data_ptr(), 2, 256, 9, H, W, 3.0, img.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(img.cpu().numpy(), ggs.render(ggs.encode(pop[:2]), H, W))
+
+
+# ---- drop-in modules -------------------------------------------------------------------------
+def test_drop_in_modules_numpy_and_torch():
+    torch = pytest.importorskip("torch")
+    from modules.fitness import fitness_many, fitness_population
+    from modules.render import render_splats_rgb_triton
+    from modules.encode import genome_to_renderer_batched
+    d = load_golden("fitness.npz")
+    H, W = (int(v) for v in d["f64__HW"])
+    pop, tgt, mask = d["f64__pop"], d["f64__target"], d["f64__mask"]
+    ref = d["f64__weighted"]
+    got = fitness_population(list(pop), tgt, H, W, 3.0, "cuda", tile=32, chunk=None,
+                             weight_mask=mask, boost_only=False)
+    assert isinstance(got, list) and len(got) == len(pop)
+    np.testing.assert_allclose(got, ref, rtol=FIT_RTOL)
+    tp = [torch.from_numpy(p).cuda() for p in pop]
+    tf = fitness_many(tp, torch.from_numpy(tgt).cuda(), H, W, 3.0, "cuda",
+                      weight_mask=torch.from_numpy(mask).cuda())
+    assert isinstance(tf, torch.Tensor) and tf.device.type == "cuda"
+    np.testing.assert_allclose(tf.cpu().numpy(), ref, rtol=FIT_RTOL)
+    g9 = genome_to_renderer_batched(torch.from_numpy(pop).cuda())
+    img = render_splats_rgb_triton(g9, H, W, k_sigma=3.0, device="cuda", tile=32)
+    assert isinstance(img, torch.Tensor) and img.shape == (len(pop), H, W, 3)
+    with pytest.raises(AssertionError):
+        render_splats_rgb_triton(g9, H, W, device="cpu")
