@@ -584,6 +584,34 @@ int ggs_preprocess(const float* genomes, int64_t S, int32_t C, int32_t H, int32_
     return stage_call(false, genomes, S, C, H, W, k_sigma, out_f9, out_i4, nullptr);
 }
 
+int ggs_detmath_eval(int32_t fn, const float* x, const float* y, int64_t n, float* out) {
+    if (fn < 0 || fn > 5) return fail(GGS_EINVAL, "bad detmath function %d", fn);
+    if (n < 0 || (n > 0 && (!x || !out || (fn == 5 && !y)))) return fail(GGS_EINVAL, "bad arguments");
+    if (n == 0) return GGS_OK;
+    int rc;
+    std::vector<DevCtx*> cs;
+    if ((rc = active_ctxs(1, &cs))) return rc;
+    DevCtx* c = cs[0];
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->dev);
+    struct Scratch {
+        void* p = nullptr;
+        ~Scratch() { if (p) (void)hipFree(p); }
+    } dx, dy, dout;
+    const size_t nb = sizeof(float) * (size_t)n;
+    GGS_HIP(hipMalloc(&dx.p, nb));
+    GGS_HIP(hipMalloc(&dout.p, nb));
+    GGS_HIP(hipMemcpy(dx.p, x, nb, hipMemcpyHostToDevice));
+    if (fn == 5) {
+        GGS_HIP(hipMalloc(&dy.p, nb));
+        GGS_HIP(hipMemcpy(dy.p, y, nb, hipMemcpyHostToDevice));
+    }
+    GGS_HIP(launch_detmath(c->stream, (const float*)dx.p, (const float*)dy.p, n, fn, (float*)dout.p));
+    GGS_HIP(hipStreamSynchronize(c->stream));
+    GGS_HIP(hipMemcpy(out, dout.p, nb, hipMemcpyDeviceToHost));
+    return GGS_OK;
+}
+
 int ggs_profile_enable(int32_t on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;

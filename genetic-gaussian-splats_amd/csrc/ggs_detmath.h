@@ -3,8 +3,8 @@
 // Device mirror of oracle/detmath.py: the same Cephes-style algorithms with the
 // same constants (given as bit patterns) and the same operation order.  This
 // translation unit is compiled with -ffp-contract=off and without fast-math, so
-// every step is one IEEE-754 binary32 add/sub/mul/div/sqrt (correctly rounded on
-// gfx950: __fdiv_rn / __fsqrt_rn), rint/floor/ceil, or an exact bit operation —
+// every step is one IEEE-754 binary32 add/sub/mul/div/sqrt (correctly rounded:
+// ggs_div_rn / ggs_sqrt_rn below), rint/floor/ceil, or an exact bit operation —
 // exactly what numpy float32 array arithmetic does.  Result: integer splat bounds
 // are bit-identical between this HIP path and the numpy oracle (SURVEY.md §7
 // "Hard parts" 1).  Domain conventions (shared with the oracle): exp(x)=0 for
@@ -40,6 +40,14 @@ constexpr float EPS6 = bitsf(0x358637BDu);   // float32(1e-6),  render.py:19-20
 constexpr float FLT_TINY = bitsf(0x00800000u);
 
 __device__ __forceinline__ bool isnan_(float x) { return x != x; }
+
+// Correctly rounded sqrt and division.  hipcc's default
+// (-fhip-fp32-correctly-rounded-divide-sqrt) lowers llvm.sqrt.f32 and fdiv to
+// IEEE-exact sequences; HIP's __fsqrt_rn is NOT (it maps to the native ~1-ulp
+// v_sqrt_f32 unless OCML_BASIC_ROUNDED_OPERATIONS is set), so it is never used.
+// tests/test_gpu_parity.py::test_detmath_bit_exact checks both against numpy.
+__device__ __forceinline__ float ggs_sqrt_rn(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float ggs_div_rn(float x, float y) { return x / y; }
 // NaN-propagating max/min/clamp (torch.clamp / np.maximum / np.clip semantics)
 __device__ __forceinline__ float nmax(float x, float lo) { return isnan_(x) ? x : (x < lo ? lo : x); }
 __device__ __forceinline__ float nclamp(float x, float lo, float hi) {

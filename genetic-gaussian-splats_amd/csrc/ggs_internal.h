@@ -26,6 +26,8 @@ int raster_tiles(int H, int W, int* nTX);
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
                          const float bg[3], float* img, const float* target, const float* mask,
                          float beta, float* partials, float* wpartials);
+hipError_t launch_detmath(hipStream_t st, const float* x, const float* y, int64_t n, int fn,
+                          float* out);
 hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,
                            int nTiles, int mode, int H, int W, float* out);
 

@@ -52,9 +52,9 @@ __device__ __forceinline__ void encode_row(const float* __restrict__ g, float ou
     const float sxx = sx2 * c2 + sy2 * s2;
     const float sxy = ((sx2 - sy2) * s) * c;
     const float syy = sx2 * s2 + sy2 * c2;
-    const float l11 = __fsqrt_rn(nmax(sxx, EPS12));
-    const float l21 = __fdiv_rn(sxy, l11);
-    const float l22 = __fsqrt_rn(nmax(syy - l21 * l21, EPS12));
+    const float l11 = ggs_sqrt_rn(nmax(sxx, EPS12));
+    const float l21 = ggs_div_rn(sxy, l11);
+    const float l22 = ggs_sqrt_rn(nmax(syy - l21 * l21, EPS12));
     out[0] = g[0];
     out[1] = g[1];
     out[2] = det_logf(l11);
@@ -79,16 +79,16 @@ __device__ __forceinline__ Prep13 preprocess_row(const float g[9], int H, int W,
     p.x1 = (int)ceilf(nclamp(p.cx + hx, 0.0f, maxx));
     p.y0 = (int)floorf(nclamp(p.cy - hy, 0.0f, maxy));
     p.y1 = (int)ceilf(nclamp(p.cy + hy, 0.0f, maxy));
-    const float i11 = __fdiv_rn(1.0f, l11);
-    const float i22 = __fdiv_rn(1.0f, l22);
+    const float i11 = ggs_div_rn(1.0f, l11);
+    const float i22 = ggs_div_rn(1.0f, l22);
     const float i21 = (-l21) * (i11 * i22);
     p.sxx = i11 * i11 + i21 * i21;
     p.sxy = i21 * i22;
     p.syy = i22 * i22;
-    p.rc = __fdiv_rn(nclamp(g[5], 0.0f, 255.0f), 255.0f);
-    p.gc = __fdiv_rn(nclamp(g[6], 0.0f, 255.0f), 255.0f);
-    p.bc = __fdiv_rn(nclamp(g[7], 0.0f, 255.0f), 255.0f);
-    p.a = __fdiv_rn(nclamp(g[8], 0.0f, 255.0f), 255.0f);
+    p.rc = ggs_div_rn(nclamp(g[5], 0.0f, 255.0f), 255.0f);
+    p.gc = ggs_div_rn(nclamp(g[6], 0.0f, 255.0f), 255.0f);
+    p.bc = ggs_div_rn(nclamp(g[7], 0.0f, 255.0f), 255.0f);
+    p.a = ggs_div_rn(nclamp(g[8], 0.0f, 255.0f), 255.0f);
     return p;
 }
 
@@ -335,6 +335,35 @@ finalize_kernel(const float* __restrict__ partials, const float* __restrict__ wp
         else v = (num / (3.0 * hw)) / (wsum / hw + 1e-12);                    // fitness.py:23-27
         out[b] = (float)v;
     }
+}
+
+// ---------------------------------------------------------------------------
+// detmath probe (parity tests of the deterministic functions, ggs_detmath_eval)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+detmath_kernel(const float* __restrict__ x, const float* __restrict__ y, int64_t n, int fn,
+               float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float a = x[i];
+    float r, s, c;
+    switch (fn) {
+        case 0: r = det_expf(a); break;
+        case 1: r = det_logf(a); break;
+        case 2: det_sincosf(a, &s, &c); r = s; break;
+        case 3: det_sincosf(a, &s, &c); r = c; break;
+        case 4: r = ggs_sqrt_rn(a); break;
+        default: r = ggs_div_rn(a, y[i]); break;
+    }
+    out[i] = r;
+}
+
+hipError_t launch_detmath(hipStream_t st, const float* x, const float* y, int64_t n, int fn,
+                          float* out) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(detmath_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, y, n,
+                       fn, out);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

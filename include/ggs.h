@@ -98,6 +98,11 @@ int ggs_encode(const float* genomes_axes, int64_t S, int32_t C, float* out_S9);
 int ggs_preprocess(const float* genomes, int64_t S, int32_t C, int32_t H, int32_t W, float k_sigma,
                    float* out_f9, int32_t* out_i4);
 
+/* Deterministic-math probe (parity tests of csrc/ggs_detmath.h against
+ * oracle/detmath.py): out[i] = f(x[i]) for fn 0 exp, 1 log, 2 sin, 3 cos,
+ * 4 sqrt (correctly rounded), 5 x[i] / y[i] (correctly rounded). */
+int ggs_detmath_eval(int32_t fn, const float* x, const float* y, int64_t n, float* out);
+
 /* ---- device-pointer API (inputs resident in HBM) ----------------------------
  * Same semantics as the host API on one device; all pointers are device
  * pointers on `device`; work is enqueued on `stream` (a hipStream_t, NULL =

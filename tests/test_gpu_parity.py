@@ -38,6 +38,49 @@ def test_device_present_and_library_native():
     assert ggs.LIB_PATH in maps
 
 
+# ---- deterministic math: bit-exact with oracle/detmath.py ---------------------------
+def _detmath(fn, x, y=None):
+    import ctypes as C
+    fp = C.POINTER(C.c_float)
+    x = np.ascontiguousarray(x, np.float32)
+    y = None if y is None else np.ascontiguousarray(y, np.float32)
+    out = np.empty_like(x)
+    rc = ggs.lib.ggs_detmath_eval(fn, x.ctypes.data_as(fp), None if y is None else y.ctypes.data_as(fp),
+                                  len(x), out.ctypes.data_as(fp))
+    assert rc == 0, ggs._lib.last_error()
+    return out
+
+
+def _specials():
+    return np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-45, 1e-38, 3.4e38, -87.0,
+                     -87.00001, 88.72283, 88.72284, 88.7229, np.pi, -np.pi, 1e7, -1e7, 1e30],
+                    np.float32)
+
+
+def test_detmath_bit_exact():
+    from detmath import exp_f32, log_f32, sincos_f32
+    rng = np.random.default_rng(0)
+    bits = rng.integers(0, 2**32, 1_000_000, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    ex = np.concatenate([rng.uniform(-95, 95, 1_000_000).astype(np.float32), _specials(), bits])
+    lg = np.concatenate([np.exp(rng.uniform(-100, 100, 1_000_000)).astype(np.float32),
+                         _specials(), np.abs(bits)])
+    tr = np.concatenate([rng.uniform(-300, 300, 1_000_000).astype(np.float32), _specials(), bits])
+    s, c = sincos_f32(tr)
+    for name, got, ref in (("exp", _detmath(0, ex), exp_f32(ex)), ("log", _detmath(1, lg), log_f32(lg)),
+                           ("sin", _detmath(2, tr), s), ("cos", _detmath(3, tr), c)):
+        same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
+        assert same.all(), (name, tr[~same][:5] if name in ("sin", "cos") else None)
+    sq = np.abs(np.concatenate([bits, rng.uniform(0, 1e6, 1_000_000).astype(np.float32)]))
+    got = _detmath(4, sq)
+    ref = np.sqrt(sq)
+    assert ((got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))).all()
+    num, den = bits, np.roll(bits, 1)
+    with np.errstate(all="ignore"):
+        ref = num / den
+    got = _detmath(5, num, den)
+    assert ((got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))).all()
+
+
 # ---- stage parity: bit-exact with the oracle ---------------------------------------
 @pytest.mark.parametrize("case", ["edge", "syn"])
 def test_encode_bit_exact_vs_oracle(case):
