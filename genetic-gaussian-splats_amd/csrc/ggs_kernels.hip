@@ -151,12 +151,27 @@ prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, f
 constexpr int TILE = 64;          // tile edge (pixels); 4 strips of 16 columns
 constexpr int RG = TILE / 4;      // row groups per lane (rows r, r+4, ...)
 constexpr int NT = 256;           // threads per workgroup
-constexpr int CAP = 512;          // LDS list capacity (records, 32 KiB)
+constexpr int CAP = 2048;         // LDS index-list capacity (splats per cull round)
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ float ufirst(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
-}
+
+#define GGS_FOR16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
+
+// One (splat, row group) pair for this lane's pixel (col, ty0 + 4g + ph):
+// e = K*quad + log2(a) (see make_rec), f = 2^e, front-to-back "over":
+//   C += T*f*c ; T *= (1 - f)       (== render.py:194-196 run back-to-front)
+// MASKED adds the per-lane row test for the AABB's first/last row block.
+#define GGS_PAIR(g, MASKED)                                                        \
+    do {                                                                           \
+        const float qy_ = qy0 + (float)(4 * (g));                                  \
+        float e_ = __builtin_fmaf(qy_, __builtin_fmaf(Cc, qy_, bx), px);           \
+        if (MASKED && (unsigned)(4 * (g) - rlo) > rspan) e_ = -__builtin_inff();   \
+        const float w_ = T##g * __builtin_amdgcn_exp2f(e_);                        \
+        R##g = __builtin_fmaf(w_, cr, R##g);                                       \
+        G##g = __builtin_fmaf(w_, cg, G##g);                                       \
+        Bl##g = __builtin_fmaf(w_, cb, Bl##g);                                     \
+        T##g = T##g - w_;                                                          \
+    } while (0)
 
 // MODE: 0 = write image, 1 = fitness/none, 2 = fitness/weighted, 3 = fitness/boost
 template <int MODE>
@@ -165,13 +180,13 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float* __restrict__ target, const float* __restrict__ mask, float beta,
               float* __restrict__ partials, float* __restrict__ wpartials) {
-    __shared__ SplatRec list[CAP];
+    __shared__ int list[CAP];
     __shared__ int wcnt[4];
     __shared__ float red[8];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wv = tid >> 6;
+    const int wv = ufirst(tid >> 6);  // wave-uniform (lets the compiler use SALU)
     const int blk = blockIdx.x;
     const int b = blk % B;            // tile-major grid: consecutive blocks share a tile
     const int t = blk / B;
@@ -186,16 +201,19 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     const float Xf = (float)col;
     const float Yb = (float)(ty0 + ph);
 
-    float R[RG], G[RG], Bl[RG], T[RG];
-#pragma unroll
-    for (int g = 0; g < RG; ++g) { R[g] = 0.0f; G[g] = 0.0f; Bl[g] = 0.0f; T[g] = 1.0f; }
+    // 16 pixels per lane x (R, G, B, transmittance), as named scalars: arrays
+    // get vectorised into <16 x float> values whose phis the allocator splits.
+#define GGS_DECL(g) float R##g = 0.0f, G##g = 0.0f, Bl##g = 0.0f, T##g = 1.0f;
+    GGS_FOR16(GGS_DECL)
+#undef GGS_DECL
 
     const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
 
     for (int base = 0; base < N; base += NT) {
-        // --- cull: splats in DESCENDING index order (front-to-back) ----------
+        // --- cull: splats in DESCENDING index order (front-to-back), ordered
+        //     compaction with wave ballots -> LDS index list ------------------
         const int i = N - 1 - (base + tid);
         bool hit = false;
         if (i >= 0) {
@@ -208,52 +226,69 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         int off = cnt;
         for (int w = 0; w < wv; ++w) off += wcnt[w];
         const int total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        if (hit) list[off + __popcll(m & lt_mask)] = crec[i];
+        if (hit) list[off + __popcll(m & lt_mask)] = i;
         cnt += total;
         __syncthreads();
         if (cnt <= CAP - NT && base + NT < N) continue;
 
-        // --- blend the list ------------------------------------------------
+        if (cnt == 0) continue;
+        // --- blend the list: splat params arrive in SGPRs (s_load_dwordx16),
+        //     the next record is fetched while the current one is blended -------
+        SplatRec nxt = crec[ufirst(list[0])];
         for (int j = 0; j < cnt; ++j) {
-            const SplatRec s = list[j];
-            const int x0 = ufirst(s.x0), x1 = ufirst(s.x1);
+            const SplatRec s = nxt;
+            nxt = crec[ufirst(list[min(j + 1, cnt - 1)])];    // unconditional: waited at the latch
+            const int x0 = s.x0, x1 = s.x1;
             if (x1 < sx0 || x0 > sx0 + 15) continue;          // strip miss (uniform)
-            const int y0 = ufirst(s.y0), y1 = ufirst(s.y1);
-            const int gA = max(y0 - ty0, 0) >> 2;
-            const int gB = min((y1 - ty0) >> 2, RG - 1);
-            const bool partA = (ty0 + 4 * gA) < y0;
-            const bool partB = (ty0 + 4 * gB + 3) > y1;
-            const float cx = ufirst(s.cx), cy = ufirst(s.cy);
-            const float A = ufirst(s.A), Bc = ufirst(s.Bc), Cc = ufirst(s.Cc), la = ufirst(s.la);
-            const float cr = ufirst(s.r), cg = ufirst(s.g), cb = ufirst(s.b);
-
-            const float qx = Xf - cx;
+            const int y0 = s.y0, y1 = s.y1;
+            const int gA = max(y0 - ty0, 0) >> 2;             // first / last row group
+            const int gB = min(y1 - ty0, TILE - 1) >> 2;
+            const float Cc = s.Cc, cr = s.r, cg = s.g, cb = s.b;
+            const float qx = Xf - s.cx;
             const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
-            const float px = inx ? __builtin_fmaf(A * qx, qx, la) : -__builtin_inff();
-            const float bx = Bc * qx;
-            const float qy0 = Yb - cy;
-#pragma unroll
-            for (int g = 0; g < RG; ++g) {
-                if (g < gA || g > gB) continue;
-                const float qy = qy0 + (float)(4 * g);
-                float e = __builtin_fmaf(qy, __builtin_fmaf(Cc, qy, bx), px);
-                if ((g == gA && partA) || (g == gB && partB)) {
-                    const int row = ty0 + 4 * g + ph;
-                    if ((unsigned)(row - y0) > (unsigned)(y1 - y0)) e = -__builtin_inff();
-                }
-                const float f = __builtin_amdgcn_exp2f(e);
-                const float w = T[g] * f;
-                R[g] = __builtin_fmaf(w, cr, R[g]);
-                G[g] = __builtin_fmaf(w, cg, G[g]);
-                Bl[g] = __builtin_fmaf(w, cb, Bl[g]);
-                T[g] = T[g] - w;
+            const float px = inx ? __builtin_fmaf(s.A * qx, qx, s.la) : -__builtin_inff();
+            const float bx = s.Bc * qx;
+            const float qy0 = Yb - s.cy;
+            const int rlo = y0 - ty0 - ph;                     // row test: 4g - rlo in [0, rspan]
+            const unsigned rspan = (unsigned)(y1 - y0);
+
+            // Duff's-device walk over the row groups gA..gB: the first and last
+            // group masked per lane, the ones in between unmasked, 2 scalar ops
+            // per group (needs -simplifycfg-sink-common=false, see Makefile).
+            switch (gA) {
+#define GGS_FIRST(g) case g: GGS_PAIR(g, true); if (gB == g) goto done; goto u##g;
+                GGS_FIRST(0) GGS_FIRST(1) GGS_FIRST(2) GGS_FIRST(3) GGS_FIRST(4)
+                GGS_FIRST(5) GGS_FIRST(6) GGS_FIRST(7) GGS_FIRST(8) GGS_FIRST(9)
+                GGS_FIRST(10) GGS_FIRST(11) GGS_FIRST(12) GGS_FIRST(13) GGS_FIRST(14)
+#undef GGS_FIRST
+                default: GGS_PAIR(15, true); goto done;
             }
+#define GGS_MID(gp, g) u##gp: if (gB == g) goto last; GGS_PAIR(g, false);
+            GGS_MID(0, 1) GGS_MID(1, 2) GGS_MID(2, 3) GGS_MID(3, 4) GGS_MID(4, 5)
+            GGS_MID(5, 6) GGS_MID(6, 7) GGS_MID(7, 8) GGS_MID(8, 9) GGS_MID(9, 10)
+            GGS_MID(10, 11) GGS_MID(11, 12) GGS_MID(12, 13) GGS_MID(13, 14)
+#undef GGS_MID
+        u14:
+        last:
+            switch (gB) {
+#define GGS_LAST(g) case g: GGS_PAIR(g, true); break;
+                GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
+                GGS_LAST(7) GGS_LAST(8) GGS_LAST(9) GGS_LAST(10) GGS_LAST(11) GGS_LAST(12)
+                GGS_LAST(13) GGS_LAST(14)
+#undef GGS_LAST
+                default: GGS_PAIR(15, true); break;
+            }
+        done:;
         }
         cnt = 0;
         __syncthreads();   // list is rewritten by the next cull round
     }
 
     // --- epilogue ---------------------------------------------------------------
+    float R[RG], G[RG], Bl[RG], T[RG];
+#define GGS_PACK(g) R[g] = R##g; G[g] = G##g; Bl[g] = Bl##g; T[g] = T##g;
+    GGS_FOR16(GGS_PACK)
+#undef GGS_PACK
     if (MODE == 0) {
         if (col < W) {
 #pragma unroll
@@ -304,6 +339,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         }
     }
 }
+#undef GGS_PAIR
 
 // ---------------------------------------------------------------------------
 // finalize: fixed-order float64 reduction of tile partials -> fitness scalar
