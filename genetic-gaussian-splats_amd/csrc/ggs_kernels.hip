@@ -151,7 +151,7 @@ prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, f
 constexpr int TILE = 64;          // tile edge (pixels); 4 strips of 16 columns
 constexpr int RG = TILE / 4;      // row groups per lane (rows r, r+4, ...)
 constexpr int NT = 256;           // threads per workgroup
-constexpr int CAP = 2048;         // LDS index-list capacity (splats per cull round)
+constexpr int CAP = 1024;         // LDS index-list capacity per strip (splats per cull round)
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -174,14 +174,15 @@ __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirst
     } while (0)
 
 // MODE: 0 = write image, 1 = fitness/none, 2 = fitness/weighted, 3 = fitness/boost
+// 96 VGPRs -> 5 waves per SIMD (64 of them are the per-lane pixel accumulators)
 template <int MODE>
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT, 5)
 raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float* __restrict__ target, const float* __restrict__ mask, float beta,
               float* __restrict__ partials, float* __restrict__ wpartials) {
-    __shared__ int list[CAP];
-    __shared__ int wcnt[4];
+    __shared__ int list[4][CAP];      // per-strip splat lists (descending index)
+    __shared__ int wcnt[4][4];        // [wave][strip] hit counts of one cull round
     __shared__ float red[8];
 
     const int tid = threadIdx.x;
@@ -209,37 +210,59 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 
     const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int cnt = 0;
+    int cnt[4] = {0, 0, 0, 0};        // per-strip list lengths (block-uniform)
 
     for (int base = 0; base < N; base += NT) {
-        // --- cull: splats in DESCENDING index order (front-to-back), ordered
-        //     compaction with wave ballots -> LDS index list ------------------
+        // --- cull: each thread tests one splat (DESCENDING index order =
+        //     front-to-back) against the 4 column strips of the tile; wave
+        //     ballots + mbcnt give an order-preserving compaction per strip ----
         const int i = N - 1 - (base + tid);
-        bool hit = false;
+        unsigned hits = 0;
         if (i >= 0) {
-            const int4 bb = *reinterpret_cast<const int4*>(&crec[i].x0);
-            hit = !(bb.y < tx0 || bb.x > tx1 || bb.w < ty0 || bb.z > ty1);
+            const int4 bb = *reinterpret_cast<const int4*>(&crec[i].x0);   // x0 x1 y0 y1
+            if (!(bb.w < ty0 || bb.z > ty1)) {
+#pragma unroll
+                for (int sidx = 0; sidx < 4; ++sidx) {
+                    const int c0 = tx0 + 16 * sidx;
+                    hits |= (unsigned)(!(bb.y < c0 || bb.x > c0 + 15)) << sidx;
+                }
+            }
         }
-        const uint64_t m = __ballot(hit);
-        if (lane == 0) wcnt[wv] = __popcll(m);
+        uint64_t m[4];
+#pragma unroll
+        for (int sidx = 0; sidx < 4; ++sidx) {
+            m[sidx] = __ballot((hits >> sidx) & 1u);
+            if (lane == 0) wcnt[wv][sidx] = __popcll(m[sidx]);
+        }
         __syncthreads();
-        int off = cnt;
-        for (int w = 0; w < wv; ++w) off += wcnt[w];
-        const int total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-        if (hit) list[off + __popcll(m & lt_mask)] = i;
-        cnt += total;
+        bool flush = base + NT >= N;
+#pragma unroll
+        for (int sidx = 0; sidx < 4; ++sidx) {
+            const int off = cnt[sidx] + (wv > 0) * wcnt[0][sidx] + (wv > 1) * wcnt[1][sidx] +
+                            (wv > 2) * wcnt[2][sidx];
+            if ((hits >> sidx) & 1u) list[sidx][off + __popcll(m[sidx] & lt_mask)] = i;
+            cnt[sidx] += wcnt[0][sidx] + wcnt[1][sidx] + wcnt[2][sidx] + wcnt[3][sidx];
+            flush |= cnt[sidx] > CAP - NT;
+        }
         __syncthreads();
-        if (cnt <= CAP - NT && base + NT < N) continue;
+        if (!flush) continue;
 
-        if (cnt == 0) continue;
-        // --- blend the list: splat params arrive in SGPRs (s_load_dwordx16),
-        //     the next record is fetched while the current one is blended -------
-        SplatRec nxt = crec[ufirst(list[0])];
-        for (int j = 0; j < cnt; ++j) {
+        // --- blend this wave's strip list: splat params arrive in SGPRs
+        //     (s_load), the next record is fetched while the current one is
+        //     blended; list indices are read 64 at a time into a VGPR (one per
+        //     lane) and picked with v_readlane (no LDS latency per splat) -------
+        // (arithmetic select: an indexed cnt[wv] makes the compiler unswitch the loop per wave)
+        const int nl = (wv == 0) * cnt[0] + (wv == 1) * cnt[1] + (wv == 2) * cnt[2] + (wv == 3) * cnt[3];
+        const int* __restrict__ mylist = &list[0][0] + wv * CAP;
+        if (nl > 0) {
+        int idxv = mylist[min(lane, nl - 1)];
+        SplatRec nxt = crec[__builtin_amdgcn_readlane(idxv, 0)];
+        for (int j = 0; j < nl; ++j) {
             const SplatRec s = nxt;
-            nxt = crec[ufirst(list[min(j + 1, cnt - 1)])];    // unconditional: waited at the latch
+            const int jn = min(j + 1, nl - 1);
+            if ((jn & 63) == 0 && jn != j) idxv = mylist[min(jn + lane, nl - 1)];
+            nxt = crec[__builtin_amdgcn_readlane(idxv, jn & 63)];   // waited at the latch
             const int x0 = s.x0, x1 = s.x1;
-            if (x1 < sx0 || x0 > sx0 + 15) continue;          // strip miss (uniform)
             const int y0 = s.y0, y1 = s.y1;
             const int gA = max(y0 - ty0, 0) >> 2;             // first / last row group
             const int gB = min(y1 - ty0, TILE - 1) >> 2;
@@ -280,8 +303,10 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             }
         done:;
         }
-        cnt = 0;
-        __syncthreads();   // list is rewritten by the next cull round
+        }
+#pragma unroll
+        for (int sidx = 0; sidx < 4; ++sidx) cnt[sidx] = 0;
+        __syncthreads();   // lists are rewritten by the next cull round
     }
 
     // --- epilogue ---------------------------------------------------------------
