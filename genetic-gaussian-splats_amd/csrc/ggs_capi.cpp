@@ -277,8 +277,9 @@ int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N,
     const int nTiles = raster_tiles(H, W, &nTX);
     int rc;
     if ((rc = ensure(w->recs, sizeof(SplatRec) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
-    if ((rc = ensure(w->partials, sizeof(float) * (size_t)(B * nTiles), st))) return rc;
-    if ((rc = ensure(w->wpartials, sizeof(float) * (size_t)nTiles, st))) return rc;
+    // one partial per (candidate, tile, 16-column strip)
+    if ((rc = ensure(w->partials, sizeof(float) * 4 * (size_t)(B * nTiles), st))) return rc;
+    if ((rc = ensure(w->wpartials, sizeof(float) * 4 * (size_t)nTiles, st))) return rc;
     SplatRec* recs = (SplatRec*)w->recs.p;
     {
         ProfScope ps(st, 0);

@@ -151,7 +151,7 @@ prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, f
 constexpr int TILE = 64;          // tile edge (pixels); 4 strips of 16 columns
 constexpr int RG = TILE / 4;      // row groups per lane (rows r, r+4, ...)
 constexpr int NT = 256;           // threads per workgroup
-constexpr int CAP = 1024;         // LDS index-list capacity per strip (splats per cull round)
+constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -174,26 +174,28 @@ __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirst
     } while (0)
 
 // MODE: 0 = write image, 1 = fitness/none, 2 = fitness/weighted, 3 = fitness/boost
-// 96 VGPRs -> 5 waves per SIMD (64 of them are the per-lane pixel accumulators)
+//
+// Workgroup = 4 independent wave64s on one 64x64 tile; wave w owns the 16-column
+// strip [tx0+16w, tx0+16w+15] x 64 rows.  No workgroup barrier anywhere: each
+// wave culls the candidate's splats against its own strip (64 per step, highest
+// index first, ballot + mbcnt compaction -> an order-preserving LDS list),
+// blends that list front-to-back, and writes its own partial sum.
+// 96 VGPRs -> 5 waves per SIMD (64 of them are the per-lane pixel accumulators).
 template <int MODE>
 __global__ void __launch_bounds__(NT, 5)
 raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float* __restrict__ target, const float* __restrict__ mask, float beta,
               float* __restrict__ partials, float* __restrict__ wpartials) {
-    __shared__ int list[4][CAP];      // per-strip splat lists (descending index)
-    __shared__ int wcnt[4][4];        // [wave][strip] hit counts of one cull round
-    __shared__ float red[8];
+    __shared__ int lists[4][CAP];     // per-wave strip lists (descending splat index)
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wv = ufirst(tid >> 6);  // wave-uniform (lets the compiler use SALU)
+    const int lane = threadIdx.x & 63;
+    const int wv = ufirst((int)(threadIdx.x >> 6));   // wave-uniform (keeps control on SALU)
     const int blk = blockIdx.x;
     const int b = blk % B;            // tile-major grid: consecutive blocks share a tile
     const int t = blk / B;
     const int tx0 = (t % nTX) * TILE;
     const int ty0 = (t / nTX) * TILE;
-    const int tx1 = min(tx0 + TILE, W) - 1;
     const int ty1 = min(ty0 + TILE, H) - 1;
 
     const int sx0 = tx0 + wv * 16;    // this wave's strip: columns [sx0, sx0+15]
@@ -209,61 +211,36 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 #undef GGS_DECL
 
     const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
+    int* __restrict__ list = &lists[0][0] + wv * CAP;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int cnt[4] = {0, 0, 0, 0};        // per-strip list lengths (block-uniform)
+    int cnt = 0;
 
-    for (int base = 0; base < N; base += NT) {
-        // --- cull: each thread tests one splat (DESCENDING index order =
-        //     front-to-back) against the 4 column strips of the tile; wave
-        //     ballots + mbcnt give an order-preserving compaction per strip ----
-        const int i = N - 1 - (base + tid);
-        unsigned hits = 0;
+    for (int base = 0; base < N; base += 64) {
+        // --- cull 64 splats (descending index = front-to-back) against the strip
+        const int i = N - 1 - (base + lane);
+        bool hit = false;
         if (i >= 0) {
             const int4 bb = *reinterpret_cast<const int4*>(&crec[i].x0);   // x0 x1 y0 y1
-            if (!(bb.w < ty0 || bb.z > ty1)) {
-#pragma unroll
-                for (int sidx = 0; sidx < 4; ++sidx) {
-                    const int c0 = tx0 + 16 * sidx;
-                    hits |= (unsigned)(!(bb.y < c0 || bb.x > c0 + 15)) << sidx;
-                }
-            }
+            hit = !(bb.w < ty0 || bb.z > ty1 || bb.y < sx0 || bb.x > sx0 + 15);
         }
-        uint64_t m[4];
-#pragma unroll
-        for (int sidx = 0; sidx < 4; ++sidx) {
-            m[sidx] = __ballot((hits >> sidx) & 1u);
-            if (lane == 0) wcnt[wv][sidx] = __popcll(m[sidx]);
-        }
-        __syncthreads();
-        bool flush = base + NT >= N;
-#pragma unroll
-        for (int sidx = 0; sidx < 4; ++sidx) {
-            const int off = cnt[sidx] + (wv > 0) * wcnt[0][sidx] + (wv > 1) * wcnt[1][sidx] +
-                            (wv > 2) * wcnt[2][sidx];
-            if ((hits >> sidx) & 1u) list[sidx][off + __popcll(m[sidx] & lt_mask)] = i;
-            cnt[sidx] += wcnt[0][sidx] + wcnt[1][sidx] + wcnt[2][sidx] + wcnt[3][sidx];
-            flush |= cnt[sidx] > CAP - NT;
-        }
-        __syncthreads();
-        if (!flush) continue;
+        const uint64_t m = __ballot(hit);
+        if (hit) list[cnt + __popcll(m & lt_mask)] = i;
+        cnt += __popcll(m);
+        if (cnt <= CAP - 64 && base + 64 < N) continue;
+        if (cnt == 0) continue;
 
-        // --- blend this wave's strip list: splat params arrive in SGPRs
-        //     (s_load), the next record is fetched while the current one is
-        //     blended; list indices are read 64 at a time into a VGPR (one per
-        //     lane) and picked with v_readlane (no LDS latency per splat) -------
-        // (arithmetic select: an indexed cnt[wv] makes the compiler unswitch the loop per wave)
-        const int nl = (wv == 0) * cnt[0] + (wv == 1) * cnt[1] + (wv == 2) * cnt[2] + (wv == 3) * cnt[3];
-        const int* __restrict__ mylist = &list[0][0] + wv * CAP;
-        if (nl > 0) {
-        int idxv = mylist[min(lane, nl - 1)];
+        // --- blend the list: splat params arrive in SGPRs (s_load), the next
+        //     record is fetched while the current one is blended; list indices
+        //     are read 64 at a time into a VGPR (one per lane) and picked with
+        //     v_readlane, so no LDS latency sits on the per-splat path ---------
+        int idxv = list[min(lane, cnt - 1)];
         SplatRec nxt = crec[__builtin_amdgcn_readlane(idxv, 0)];
-        for (int j = 0; j < nl; ++j) {
+        for (int j = 0; j < cnt; ++j) {
             const SplatRec s = nxt;
-            const int jn = min(j + 1, nl - 1);
-            if ((jn & 63) == 0 && jn != j) idxv = mylist[min(jn + lane, nl - 1)];
+            const int jn = min(j + 1, cnt - 1);
+            if ((jn & 63) == 0 && jn != j) idxv = list[min(jn + lane, cnt - 1)];
             nxt = crec[__builtin_amdgcn_readlane(idxv, jn & 63)];   // waited at the latch
-            const int x0 = s.x0, x1 = s.x1;
-            const int y0 = s.y0, y1 = s.y1;
+            const int x0 = s.x0, x1 = s.x1, y0 = s.y0, y1 = s.y1;
             const int gA = max(y0 - ty0, 0) >> 2;             // first / last row group
             const int gB = min(y1 - ty0, TILE - 1) >> 2;
             const float Cc = s.Cc, cr = s.r, cg = s.g, cb = s.b;
@@ -303,10 +280,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             }
         done:;
         }
-        }
-#pragma unroll
-        for (int sidx = 0; sidx < 4; ++sidx) cnt[sidx] = 0;
-        __syncthreads();   // lists are rewritten by the next cull round
+        cnt = 0;
     }
 
     // --- epilogue ---------------------------------------------------------------
@@ -327,7 +301,6 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
                 }
             }
         }
-        return;
     } else {
         float acc = 0.0f, wacc = 0.0f;
         if (col < W) {
@@ -356,11 +329,9 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             acc += __shfl_xor(acc, o);
             wacc += __shfl_xor(wacc, o);
         }
-        if (lane == 0) { red[wv] = acc; red[4 + wv] = wacc; }
-        __syncthreads();
-        if (tid == 0) {
-            partials[(int64_t)b * nTiles + t] = (red[0] + red[1]) + (red[2] + red[3]);
-            if (b == 0 && wpartials) wpartials[t] = (red[4] + red[5]) + (red[6] + red[7]);
+        if (lane == 0) {      // one partial per (candidate, tile, strip): no block barrier
+            partials[((int64_t)b * nTiles + t) * 4 + wv] = acc;
+            if (b == 0 && wpartials) wpartials[t * 4 + wv] = wacc;
         }
     }
 }
@@ -470,7 +441,8 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, 
 
 hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,
                            int nTiles, int mode, int H, int W, float* out) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(B), dim3(256), 0, st, partials, wpartials, nTiles, mode,
+    // 4 strip partials per (candidate, tile)
+    hipLaunchKernelGGL(finalize_kernel, dim3(B), dim3(256), 0, st, partials, wpartials, nTiles * 4, mode,
                        (double)H * (double)W, out);
     return hipGetLastError();
 }
