@@ -161,17 +161,56 @@ __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirst
 // e = K*quad + log2(a) (see make_rec), f = 2^e, front-to-back "over":
 //   C += T*f*c ; T *= (1 - f)       (== render.py:194-196 run back-to-front)
 // MASKED adds the per-lane row test for the AABB's first/last row block.
+// Performance-ablation switch (tools/ablate.py; 0 in every shipped build):
+// 1 = exp replaced by a multiply, 2 = no row-group bodies, 3 = red channel only.
+#ifndef GGS_ABL
+#define GGS_ABL 0
+#endif
+#if GGS_ABL == 1
+#define GGS_EXP2(x) ((x) * 0.0001f)
+#else
+#define GGS_EXP2(x) __builtin_amdgcn_exp2f(x)
+#endif
 #define GGS_PAIR(g, MASKED)                                                        \
     do {                                                                           \
+        if (GGS_ABL == 2) break;                                                   \
         const float qy_ = qy0 + (float)(4 * (g));                                  \
         float e_ = __builtin_fmaf(qy_, __builtin_fmaf(Cc, qy_, bx), px);           \
         if (MASKED && (unsigned)(4 * (g) - rlo) > rspan) e_ = -__builtin_inff();   \
-        const float w_ = T##g * __builtin_amdgcn_exp2f(e_);                        \
+        const float w_ = T##g * GGS_EXP2(e_);                                      \
         R##g = __builtin_fmaf(w_, cr, R##g);                                       \
-        G##g = __builtin_fmaf(w_, cg, G##g);                                       \
-        Bl##g = __builtin_fmaf(w_, cb, Bl##g);                                     \
+        if (GGS_ABL != 3) G##g = __builtin_fmaf(w_, cg, G##g);                     \
+        if (GGS_ABL != 3) Bl##g = __builtin_fmaf(w_, cb, Bl##g);                   \
         T##g = T##g - w_;                                                          \
     } while (0)
+
+// Packed variant (GGS_PACKED): two adjacent row groups (2k, 2k+1) per lane in
+// one float2, so qy / the quadratic / the blend run as v_pk_{add,fma,mul}_f32
+// (2 FP32 ops per lane per issue); the exp stays per element.
+#ifndef GGS_PACKED
+#define GGS_PACKED 1
+#endif
+typedef float f2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_elementwise_fma(a, b, c); }
+#define GGS_PK(k, MASKED)                                                            \
+    do {                                                                             \
+        if (GGS_ABL == 2) break;                                                     \
+        const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                   \
+        f2_t e_ = fma2(qy_, fma2(Cc2, qy_, bx2), px2);                               \
+        if (MASKED) {                                                                \
+            if ((unsigned)(8 * (k) - rlo) > rspan) e_.x = -__builtin_inff();         \
+            if ((unsigned)(8 * (k) + 4 - rlo) > rspan) e_.y = -__builtin_inff();     \
+        }                                                                            \
+        f2_t f_;                                                                     \
+        f_.x = GGS_EXP2(e_.x);                                                       \
+        f_.y = GGS_EXP2(e_.y);                                                       \
+        const f2_t w_ = P_T##k * f_;                                                 \
+        P_R##k = fma2(w_, cr2, P_R##k);                                              \
+        if (GGS_ABL != 3) P_G##k = fma2(w_, cg2, P_G##k);                            \
+        if (GGS_ABL != 3) P_B##k = fma2(w_, cb2, P_B##k);                            \
+        P_T##k = P_T##k - w_;                                                        \
+    } while (0)
+#define GGS_FOR8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 
 // MODE: 0 = write image, 1 = fitness/none, 2 = fitness/weighted, 3 = fitness/boost
 //
@@ -206,8 +245,13 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 
     // 16 pixels per lane x (R, G, B, transmittance), as named scalars: arrays
     // get vectorised into <16 x float> values whose phis the allocator splits.
+#if GGS_PACKED
+#define GGS_DECL(k) f2_t P_R##k = 0.0f, P_G##k = 0.0f, P_B##k = 0.0f, P_T##k = 1.0f;
+    GGS_FOR8(GGS_DECL)
+#else
 #define GGS_DECL(g) float R##g = 0.0f, G##g = 0.0f, Bl##g = 0.0f, T##g = 1.0f;
     GGS_FOR16(GGS_DECL)
+#endif
 #undef GGS_DECL
 
     const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
@@ -252,6 +296,30 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             const int rlo = y0 - ty0 - ph;                     // row test: 4g - rlo in [0, rspan]
             const unsigned rspan = (unsigned)(y1 - y0);
 
+#if GGS_PACKED
+            const f2_t qyv = {qy0, qy0 + 4.0f}, Cc2 = Cc, bx2 = bx, px2 = px;
+            const f2_t cr2 = cr, cg2 = cg, cb2 = cb;
+            const int kA = gA >> 1, kB = gB >> 1;             // first / last group pair
+            switch (kA) {
+#define GGS_FIRST(k) case k: GGS_PK(k, true); if (kB == k) goto done; goto u##k;
+                GGS_FIRST(0) GGS_FIRST(1) GGS_FIRST(2) GGS_FIRST(3) GGS_FIRST(4)
+                GGS_FIRST(5) GGS_FIRST(6)
+#undef GGS_FIRST
+                default: GGS_PK(7, true); goto done;
+            }
+#define GGS_MID(kp, k) u##kp: if (kB == k) goto last; GGS_PK(k, false);
+            GGS_MID(0, 1) GGS_MID(1, 2) GGS_MID(2, 3) GGS_MID(3, 4) GGS_MID(4, 5)
+            GGS_MID(5, 6)
+#undef GGS_MID
+        u6:
+        last:
+            switch (kB) {
+#define GGS_LAST(k) case k: GGS_PK(k, true); break;
+                GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
+#undef GGS_LAST
+                default: GGS_PK(7, true); break;
+            }
+#else
             // Duff's-device walk over the row groups gA..gB: the first and last
             // group masked per lane, the ones in between unmasked, 2 scalar ops
             // per group (needs -simplifycfg-sink-common=false, see Makefile).
@@ -278,15 +346,27 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 #undef GGS_LAST
                 default: GGS_PAIR(15, true); break;
             }
+#endif
         done:;
+#if GGS_ABL == 2
+            asm volatile("" :: "v"(px), "v"(bx), "v"(qy0), "v"(rlo), "s"(rspan), "s"(Cc), "s"(cr),
+                         "s"(cg), "s"(cb), "s"(gA), "s"(gB));
+#endif
         }
         cnt = 0;
     }
 
     // --- epilogue ---------------------------------------------------------------
     float R[RG], G[RG], Bl[RG], T[RG];
+#if GGS_PACKED
+#define GGS_PACK(k)                                                   \
+    R[2 * k] = P_R##k.x; G[2 * k] = P_G##k.x; Bl[2 * k] = P_B##k.x; T[2 * k] = P_T##k.x; \
+    R[2 * k + 1] = P_R##k.y; G[2 * k + 1] = P_G##k.y; Bl[2 * k + 1] = P_B##k.y; T[2 * k + 1] = P_T##k.y;
+    GGS_FOR8(GGS_PACK)
+#else
 #define GGS_PACK(g) R[g] = R##g; G[g] = G##g; Bl[g] = Bl##g; T[g] = T##g;
     GGS_FOR16(GGS_PACK)
+#endif
 #undef GGS_PACK
     if (MODE == 0) {
         if (col < W) {
