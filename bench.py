@@ -57,6 +57,21 @@ def synthetic_population(B, N, seed):
     return G
 
 
+def pmc_traffic():
+    """HBM bytes per raster launch from the newest committed rocprofv3 PMC
+    summary of this same workload (tools/profile.sh -> profiles/rNN/summary.json:
+    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE); None when absent."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "summary.json")))
+    if not paths:
+        return None, None
+    try:
+        d = json.load(open(paths[-1]))
+        return d["raster_hbm_bytes_per_launch"]["total"], os.path.relpath(paths[-1], REPO)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def _cpu_worker(args):
     pop, tgt, mask = args
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -170,6 +185,7 @@ def main():
     raster_bytes = BYTES_PER_CANDIDATE * POP
     achieved_gbs = raster_bytes / (raster_ms * 1e-3) / 1e9
     valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic()
     if rank == 0:
         line = {
             "metric": "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=128",
@@ -192,7 +208,9 @@ def main():
             "aabb_pairs_per_s": round(value * pairs_per_cand, 1),
             "roofline": {"bound": "hbm", "kernel": "raster_kernel<2>",
                          "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": raster_bytes,
                          "avg_launch_ms": round(raster_ms, 5),
                          "note": "VALU/transcendental-bound path (SURVEY.md §8d): see 'valu'"},

@@ -85,8 +85,25 @@ int ensure_pinned(PinBuf& b, size_t bytes) {
 // Per-(device, stream) scratch used by one render/fitness pipeline.
 struct Workspace {
     hipStream_t stream = nullptr;
-    DevBuf recs, partials, wpartials;
+    DevBuf recs, partials, wpartials, order;
+    int order_H = -1, order_W = -1;   // (H, W) the tile order was built for
 };
+
+// Upload the central-tiles-first raster order for (H, W) once per size.
+int ensure_tile_order(Workspace* w, int H, int W, hipStream_t st) {
+    if (w->order_H == H && w->order_W == W) return GGS_OK;
+    int nTX;
+    const int n = raster_tiles(H, W, &nTX);
+    int rc;
+    if ((rc = ensure(w->order, sizeof(int) * (size_t)n, st))) return rc;
+    std::vector<int> h(n);
+    raster_tile_order(H, W, h.data());
+    GGS_HIP(hipStreamSynchronize(st));
+    GGS_HIP(hipMemcpy(w->order.p, h.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    w->order_H = H;
+    w->order_W = W;
+    return GGS_OK;
+}
 
 struct DevCtx {
     int dev = 0;
@@ -280,6 +297,7 @@ int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N,
     // one partial per (candidate, tile, 16-column strip)
     if ((rc = ensure(w->partials, sizeof(float) * 4 * (size_t)(B * nTiles), st))) return rc;
     if ((rc = ensure(w->wpartials, sizeof(float) * 4 * (size_t)nTiles, st))) return rc;
+    if ((rc = ensure_tile_order(w, H, W, st))) return rc;
     SplatRec* recs = (SplatRec*)w->recs.p;
     {
         ProfScope ps(st, 0);
@@ -289,7 +307,7 @@ int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N,
     {
         ProfScope ps(st, 1);
         GGS_HIP(launch_raster(st, 1 + mode, recs, (int)B, N, H, W, bg, nullptr, d_target, d_mask, beta,
-                              (float*)w->partials.p, (float*)w->wpartials.p));
+                              (float*)w->partials.p, (float*)w->wpartials.p, (const int*)w->order.p));
     }
     {
         ProfScope ps(st, 2);
@@ -305,6 +323,7 @@ int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, 
     Workspace* w = workspace_for(c, st);
     int rc;
     if ((rc = ensure(w->recs, sizeof(SplatRec) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
+    if ((rc = ensure_tile_order(w, H, W, st))) return rc;
     SplatRec* recs = (SplatRec*)w->recs.p;
     {
         ProfScope ps(st, 0);
@@ -313,7 +332,7 @@ int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, 
     {
         ProfScope ps(st, 1);
         GGS_HIP(launch_raster(st, 0, recs, (int)B, N, H, W, bg, d_img, nullptr, nullptr, 0.f, nullptr,
-                              nullptr));
+                              nullptr, (const int*)w->order.p));
     }
     return GGS_OK;
 }
@@ -378,7 +397,7 @@ void ggs_shutdown(void) {
         (void)hipStreamSynchronize(c->stream);
         for (auto& w : c->ws) {
             if (w->stream) (void)hipStreamSynchronize(w->stream);
-            for (DevBuf* b : {&w->recs, &w->partials, &w->wpartials})
+            for (DevBuf* b : {&w->recs, &w->partials, &w->wpartials, &w->order})
                 if (b->p) (void)hipFree(b->p);
         }
         for (DevBuf* b : {&c->gen, &c->out, &c->target, &c->mask})

@@ -25,7 +25,11 @@ hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_
 int raster_tiles(int H, int W, int* nTX);
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
                          const float bg[3], float* img, const float* target, const float* mask,
-                         float beta, float* partials, float* wpartials);
+                         float beta, float* partials, float* wpartials, const int* tile_order);
+// Tile visiting order for the raster grid: tiles sorted by distance of their
+// centre from the image centre (central tiles carry the most splats; running
+// them first shortens the tail of the launch).
+void raster_tile_order(int H, int W, int* order);
 hipError_t launch_detmath(hipStream_t st, const float* x, const float* y, int64_t n, int fn,
                           float* out);
 hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,

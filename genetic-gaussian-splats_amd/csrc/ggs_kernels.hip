@@ -26,6 +26,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <utility>
+#include <vector>
+
 #include "ggs_detmath.h"
 #include "ggs_internal.h"
 
@@ -225,14 +229,15 @@ __global__ void __launch_bounds__(NT, 5)
 raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float* __restrict__ target, const float* __restrict__ mask, float beta,
-              float* __restrict__ partials, float* __restrict__ wpartials) {
+              float* __restrict__ partials, float* __restrict__ wpartials,
+              const int* __restrict__ tile_order) {
     __shared__ int lists[4][CAP];     // per-wave strip lists (descending splat index)
 
     const int lane = threadIdx.x & 63;
     const int wv = ufirst((int)(threadIdx.x >> 6));   // wave-uniform (keeps control on SALU)
     const int blk = blockIdx.x;
     const int b = blk % B;            // tile-major grid: consecutive blocks share a tile
-    const int t = blk / B;
+    const int t = tile_order ? tile_order[blk / B] : blk / B;   // heavy (central) tiles first
     const int tx0 = (t % nTX) * TILE;
     const int ty0 = (t / nTX) * TILE;
     const int ty1 = min(ty0 + TILE, H) - 1;
@@ -494,6 +499,19 @@ hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_
     return hipGetLastError();
 }
 
+void raster_tile_order(int H, int W, int* order) {
+    int nTX;
+    const int n = raster_tiles(H, W, &nTX);
+    std::vector<std::pair<double, int>> d(n);
+    for (int t = 0; t < n; ++t) {
+        const double cx = (t % nTX) * TILE + 0.5 * TILE - 0.5 * W;
+        const double cy = (t / nTX) * TILE + 0.5 * TILE - 0.5 * H;
+        d[t] = {cx * cx + cy * cy, t};
+    }
+    std::stable_sort(d.begin(), d.end());
+    for (int t = 0; t < n; ++t) order[t] = d[t].second;
+}
+
 int raster_tiles(int H, int W, int* nTX) {
     const int tx = (W + TILE - 1) / TILE, ty = (H + TILE - 1) / TILE;
     if (nTX) *nTX = tx;
@@ -502,13 +520,13 @@ int raster_tiles(int H, int W, int* nTX) {
 
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
                          const float bg[3], float* img, const float* target, const float* mask,
-                         float beta, float* partials, float* wpartials) {
+                         float beta, float* partials, float* wpartials, const int* tile_order) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles)), block(NT);
 #define GGS_RASTER(M)                                                                          \
     hipLaunchKernelGGL(raster_kernel<M>, grid, block, 0, st, recs, B, N, H, W, nTX, nTiles,     \
-                       bg[0], bg[1], bg[2], img, target, mask, beta, partials, wpartials)
+                       bg[0], bg[1], bg[2], img, target, mask, beta, partials, wpartials, tile_order)
     switch (mode) {
         case 0: GGS_RASTER(0); break;
         case 1: GGS_RASTER(1); break;
