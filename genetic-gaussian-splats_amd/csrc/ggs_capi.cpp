@@ -278,9 +278,9 @@ int check_dims(int64_t B, int32_t N, int32_t C, int32_t H, int32_t W) {
     if (H < 1 || W < 1) return fail(GGS_EINVAL, "H=%d, W=%d must be >= 1", H, W);
     int nTX;
     const int64_t nTiles = raster_tiles(H, W, &nTX);
-    if (B * nTiles >= (int64_t)1 << 31)
+    if (B * nTiles * 4 >= (int64_t)1 << 31)
         return fail(GGS_EINVAL, "B*tiles = %lld exceeds the grid limit; split the batch",
-                    (long long)(B * nTiles));
+                    (long long)(B * nTiles * 4));
     return GGS_OK;
 }
 

@@ -152,9 +152,19 @@ prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, f
 // ---------------------------------------------------------------------------
 // raster
 // ---------------------------------------------------------------------------
-constexpr int TILE = 64;          // tile edge (pixels); 4 strips of 16 columns
-constexpr int RG = TILE / 4;      // row groups per lane (rows r, r+4, ...)
-constexpr int NT = 256;           // threads per workgroup
+#ifndef GGS_ROWS
+#define GGS_ROWS 64
+#endif
+constexpr int TILE = 64;          // tile width (pixels): 4 strips of 16 columns
+constexpr int TILE_H = GGS_ROWS;  // tile height (rows); one wave covers a 16 x TILE_H strip
+constexpr int RG = TILE_H / 4;    // row groups per lane (rows r, r+4, ...)
+constexpr int NPK = RG / 2;       // packed row-group pairs per lane
+#ifndef GGS_WPB
+#define GGS_WPB 1
+#endif
+constexpr int WPB = GGS_WPB;      // waves per workgroup (each wave owns one 16-column strip)
+constexpr int NT = 64 * WPB;      // threads per workgroup
+constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -231,16 +241,17 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
               const float* __restrict__ target, const float* __restrict__ mask, float beta,
               float* __restrict__ partials, float* __restrict__ wpartials,
               const int* __restrict__ tile_order) {
-    __shared__ int lists[4][CAP];     // per-wave strip lists (descending splat index)
+    __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
 
     const int lane = threadIdx.x & 63;
-    const int wv = ufirst((int)(threadIdx.x >> 6));   // wave-uniform (keeps control on SALU)
-    const int blk = blockIdx.x;
+    const int wib = ufirst((int)(threadIdx.x >> 6));  // wave in block (uniform: keeps control on SALU)
+    const int blk = blockIdx.x / SPB;
+    const int wv = (blockIdx.x % SPB) * WPB + wib;    // strip 0..3 of the tile
     const int b = blk % B;            // tile-major grid: consecutive blocks share a tile
     const int t = tile_order ? tile_order[blk / B] : blk / B;   // heavy (central) tiles first
     const int tx0 = (t % nTX) * TILE;
-    const int ty0 = (t / nTX) * TILE;
-    const int ty1 = min(ty0 + TILE, H) - 1;
+    const int ty0 = (t / nTX) * TILE_H;
+    const int ty1 = min(ty0 + TILE_H, H) - 1;
 
     const int sx0 = tx0 + wv * 16;    // this wave's strip: columns [sx0, sx0+15]
     const int col = sx0 + (lane & 15);
@@ -260,7 +271,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 #undef GGS_DECL
 
     const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
-    int* __restrict__ list = &lists[0][0] + wv * CAP;
+    int* __restrict__ list = &lists[0][0] + wib * CAP;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
 
@@ -291,7 +302,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             nxt = crec[__builtin_amdgcn_readlane(idxv, jn & 63)];   // waited at the latch
             const int x0 = s.x0, x1 = s.x1, y0 = s.y0, y1 = s.y1;
             const int gA = max(y0 - ty0, 0) >> 2;             // first / last row group
-            const int gB = min(y1 - ty0, TILE - 1) >> 2;
+            const int gB = min(y1 - ty0, TILE_H - 1) >> 2;
             const float Cc = s.Cc, cr = s.r, cg = s.g, cb = s.b;
             const float qx = Xf - s.cx;
             const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
@@ -306,50 +317,55 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             const f2_t cr2 = cr, cg2 = cg, cb2 = cb;
             const int kA = gA >> 1, kB = gB >> 1;             // first / last group pair
             switch (kA) {
-#define GGS_FIRST(k) case k: GGS_PK(k, true); if (kB == k) goto done; goto u##k;
+#define GGS_FIRST(k) \
+    case k: if (k < NPK) { GGS_PK(k, true); if (kB == k) goto done; goto u##k; } break;
                 GGS_FIRST(0) GGS_FIRST(1) GGS_FIRST(2) GGS_FIRST(3) GGS_FIRST(4)
-                GGS_FIRST(5) GGS_FIRST(6)
+                GGS_FIRST(5) GGS_FIRST(6) GGS_FIRST(7)
 #undef GGS_FIRST
-                default: GGS_PK(7, true); goto done;
+                default: __builtin_unreachable();
             }
-#define GGS_MID(kp, k) u##kp: if (kB == k) goto last; GGS_PK(k, false);
+#define GGS_MID(kp, k) u##kp: if (kB == k) goto last; if (k < NPK) GGS_PK(k, false);
             GGS_MID(0, 1) GGS_MID(1, 2) GGS_MID(2, 3) GGS_MID(3, 4) GGS_MID(4, 5)
-            GGS_MID(5, 6)
+            GGS_MID(5, 6) GGS_MID(6, 7)
 #undef GGS_MID
-        u6:
+        u7:
         last:
             switch (kB) {
-#define GGS_LAST(k) case k: GGS_PK(k, true); break;
+#define GGS_LAST(k) case k: if (k < NPK) GGS_PK(k, true); break;
                 GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
+                GGS_LAST(7)
 #undef GGS_LAST
-                default: GGS_PK(7, true); break;
+                default: __builtin_unreachable();
             }
 #else
             // Duff's-device walk over the row groups gA..gB: the first and last
             // group masked per lane, the ones in between unmasked, 2 scalar ops
             // per group (needs -simplifycfg-sink-common=false, see Makefile).
             switch (gA) {
-#define GGS_FIRST(g) case g: GGS_PAIR(g, true); if (gB == g) goto done; goto u##g;
+#define GGS_FIRST(g) \
+    case g: if (g < RG) { GGS_PAIR(g, true); if (gB == g) goto done; goto u##g; } break;
                 GGS_FIRST(0) GGS_FIRST(1) GGS_FIRST(2) GGS_FIRST(3) GGS_FIRST(4)
                 GGS_FIRST(5) GGS_FIRST(6) GGS_FIRST(7) GGS_FIRST(8) GGS_FIRST(9)
                 GGS_FIRST(10) GGS_FIRST(11) GGS_FIRST(12) GGS_FIRST(13) GGS_FIRST(14)
+                GGS_FIRST(15)
 #undef GGS_FIRST
-                default: GGS_PAIR(15, true); goto done;
+                default: __builtin_unreachable();
             }
-#define GGS_MID(gp, g) u##gp: if (gB == g) goto last; GGS_PAIR(g, false);
+#define GGS_MID(gp, g) u##gp: if (gB == g) goto last; if (g < RG) GGS_PAIR(g, false);
             GGS_MID(0, 1) GGS_MID(1, 2) GGS_MID(2, 3) GGS_MID(3, 4) GGS_MID(4, 5)
             GGS_MID(5, 6) GGS_MID(6, 7) GGS_MID(7, 8) GGS_MID(8, 9) GGS_MID(9, 10)
             GGS_MID(10, 11) GGS_MID(11, 12) GGS_MID(12, 13) GGS_MID(13, 14)
 #undef GGS_MID
-        u14:
+            GGS_MID(14, 15)
+        u15:
         last:
             switch (gB) {
-#define GGS_LAST(g) case g: GGS_PAIR(g, true); break;
+#define GGS_LAST(g) case g: if (g < RG) GGS_PAIR(g, true); break;
                 GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
                 GGS_LAST(7) GGS_LAST(8) GGS_LAST(9) GGS_LAST(10) GGS_LAST(11) GGS_LAST(12)
-                GGS_LAST(13) GGS_LAST(14)
+                GGS_LAST(13) GGS_LAST(14) GGS_LAST(15)
 #undef GGS_LAST
-                default: GGS_PAIR(15, true); break;
+                default: __builtin_unreachable();
             }
 #endif
         done:;
@@ -364,12 +380,15 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     // --- epilogue ---------------------------------------------------------------
     float R[RG], G[RG], Bl[RG], T[RG];
 #if GGS_PACKED
-#define GGS_PACK(k)                                                   \
-    R[2 * k] = P_R##k.x; G[2 * k] = P_G##k.x; Bl[2 * k] = P_B##k.x; T[2 * k] = P_T##k.x; \
-    R[2 * k + 1] = P_R##k.y; G[2 * k + 1] = P_G##k.y; Bl[2 * k + 1] = P_B##k.y; T[2 * k + 1] = P_T##k.y;
+#define GGS_PACK(k)                                                                   \
+    if (k < NPK) {                                                                    \
+        R[2 * k] = P_R##k.x; G[2 * k] = P_G##k.x; Bl[2 * k] = P_B##k.x; T[2 * k] = P_T##k.x; \
+        R[2 * k + 1] = P_R##k.y; G[2 * k + 1] = P_G##k.y; Bl[2 * k + 1] = P_B##k.y;   \
+        T[2 * k + 1] = P_T##k.y;                                                      \
+    }
     GGS_FOR8(GGS_PACK)
 #else
-#define GGS_PACK(g) R[g] = R##g; G[g] = G##g; Bl[g] = Bl##g; T[g] = T##g;
+#define GGS_PACK(g) if (g < RG) { R[g] = R##g; G[g] = G##g; Bl[g] = Bl##g; T[g] = T##g; }
     GGS_FOR16(GGS_PACK)
 #endif
 #undef GGS_PACK
@@ -505,7 +524,7 @@ void raster_tile_order(int H, int W, int* order) {
     std::vector<std::pair<double, int>> d(n);
     for (int t = 0; t < n; ++t) {
         const double cx = (t % nTX) * TILE + 0.5 * TILE - 0.5 * W;
-        const double cy = (t / nTX) * TILE + 0.5 * TILE - 0.5 * H;
+        const double cy = (t / nTX) * TILE_H + 0.5 * TILE_H - 0.5 * H;
         d[t] = {cx * cx + cy * cy, t};
     }
     std::stable_sort(d.begin(), d.end());
@@ -513,7 +532,7 @@ void raster_tile_order(int H, int W, int* order) {
 }
 
 int raster_tiles(int H, int W, int* nTX) {
-    const int tx = (W + TILE - 1) / TILE, ty = (H + TILE - 1) / TILE;
+    const int tx = (W + TILE - 1) / TILE, ty = (H + TILE_H - 1) / TILE_H;
     if (nTX) *nTX = tx;
     return tx * ty;
 }
@@ -523,7 +542,7 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, 
                          float beta, float* partials, float* wpartials, const int* tile_order) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
-    const dim3 grid((unsigned)((int64_t)B * nTiles)), block(NT);
+    const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
 #define GGS_RASTER(M)                                                                          \
     hipLaunchKernelGGL(raster_kernel<M>, grid, block, 0, st, recs, B, N, H, W, nTX, nTiles,     \
                        bg[0], bg[1], bg[2], img, target, mask, beta, partials, wpartials, tile_order)
