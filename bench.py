@@ -29,6 +29,10 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "genetic-gaussian-splats_amd"))
 
+# BASELINE.json configs: [1] is the metric's workload (default); [2] is the
+# 1024^2 / 1024-splat / pop-512 single-GPU case (--config 1024), whose per-GPU
+# shard is also configs[3] (pop 4096 over 8 GPUs = 512 per GPU).
+CONFIGS = {"512": (512, 256, 128), "1024": (1024, 1024, 512)}
 H = W = 512
 N_SPLATS = 256
 POP = 128
@@ -37,8 +41,11 @@ N_POPS = 4
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: peak FP32 vector
 FLOP_PER_PAIR = 24
-# algorithmic bytes per candidate, fused fitness = 12HW + 4HW + 36N + 4
-BYTES_PER_CANDIDATE = 12 * H * W + 4 * H * W + 36 * N_SPLATS + 4
+
+
+def bytes_per_candidate():
+    """algorithmic bytes per candidate, fused fitness = 12HW + 4HW + 36N + 4."""
+    return 12 * H * W + 4 * H * W + 36 * N_SPLATS + 4
 
 
 def synthetic_population(B, N, seed):
@@ -104,7 +111,11 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="512")
     args = ap.parse_args()
+    global H, W, N_SPLATS, POP
+    H, N_SPLATS, POP = CONFIGS[args.config]
+    W = H
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -115,7 +126,7 @@ def main():
     mask_h = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "512":
         cpu = cpu_baseline(tgt_h, mask_h)
 
     import torch
@@ -124,7 +135,8 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ   # torchrun, even at N=1
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     pops = [torch.from_numpy(synthetic_population(POP, N_SPLATS, 10_000 * rank + i)).to(dev)
@@ -140,11 +152,11 @@ def main():
         g = pops[i % N_POPS]
         ggs.fitness_device(local_rank, st, g.data_ptr(), POP, N_SPLATS, 9, tgt.data_ptr(),
                            mask.data_ptr(), ggs.GGS_FIT_WEIGHTED, 1.0, H, W, K_SIGMA, out.data_ptr())
-        if world > 1:
+        if distributed:
             dist.all_gather_into_tensor(gathered, out)      # RCCL: fitness scalars to every rank
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
@@ -156,7 +168,7 @@ def main():
         step(i)
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -182,13 +194,15 @@ def main():
 
     total = world * POP * args.steps
     value = total / elapsed
-    raster_bytes = BYTES_PER_CANDIDATE * POP
+    raster_bytes = bytes_per_candidate() * POP
     achieved_gbs = raster_bytes / (raster_ms * 1e-3) / 1e9
     valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic()
+    traffic, traffic_src = pmc_traffic() if args.config == "512" else (None, None)
     if rank == 0:
         line = {
-            "metric": "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=128",
+            "metric": "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=128"
+                      if args.config == "512" else
+                      f"candidate renders/sec, {H}x{W}, {N_SPLATS} splats, pop={POP} per GPU",
             "value": round(value, 1),
             "unit": "candidate renders/s",
             "n_gpus": world,
@@ -200,7 +214,7 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (population.py distributions, U[0,1] target, U[0.405,1] mask)",
-            "config": {"workload": "512x512 canvas, 256 splats/candidate, pop=128 per GPU, "
+            "config": {"workload": f"{H}x{W} canvas, {N_SPLATS} splats/candidate, pop={POP} per GPU, "
                                    "weighted-L2 fitness (encode+prep+raster+reduce)",
                        "H": H, "W": W, "splats": N_SPLATS, "pop_per_gpu": POP,
                        "global_batch": POP * world, "parallelism": f"dp{world} (candidate shards)"},
@@ -221,7 +235,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

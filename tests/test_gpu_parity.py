@@ -190,6 +190,22 @@ def test_fitness_vs_oracle_512():
                                    O.fitness_many(list(pop), tgt, H, W, 3.0, **kw), rtol=FIT_RTOL)
 
 
+def test_fitness_vs_oracle_1024_config():
+    """configs[2]/[3] shape: 1024^2, 1024 splats (two candidates vs the oracle) and
+    the batch invariance of the full pop-512 evaluation."""
+    H = W = 1024
+    pop = O.synthetic_population(512, 1024, H, W, seed=31)
+    rng = np.random.default_rng(6)
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
+    full = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+    idx = [0, 511]
+    np.testing.assert_allclose(full[idx], O.fitness_many(list(pop[idx]), tgt, H, W, 3.0,
+                                                         weight_mask=mask), rtol=FIT_RTOL)
+    np.testing.assert_array_equal(full[200:264], ggs.fitness(pop[200:264], tgt, H, W, 3.0,
+                                                             weight_mask=mask))
+
+
 # ---- full-size properties (512^2 / 256 splats / pop 128) -------------------------------------
 @pytest.fixture(scope="module")
 def full_size():
