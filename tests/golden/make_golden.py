@@ -203,6 +203,20 @@ def main() -> None:
         mk[f"mask_s{strength}"] = M.compute_importance_mask(
             t(tgt), 96, 80, edge_scales=(1, 2, 4), w_edge=0.7, w_var=0.3, gamma=0.7,
             floor=0.15, smooth=3, strength=strength).numpy()
+    # resize inside the mask (target 100x70 -> mask 64x48) and the GA's target prep
+    # (algorithm.py:33-39: /255 when max > 1.5, bilinear align_corners=False)
+    tgt2 = np.random.default_rng(8).uniform(0, 255, (100, 70, 3)).astype(np.float32)
+    mk["target_u8"] = tgt2
+    mk["mask_resized_64x48"] = M.compute_importance_mask(
+        t(tgt2), 64, 48, edge_scales=(1, 2, 4), w_edge=0.7, w_var=0.3, gamma=0.7,
+        floor=0.15, smooth=3, strength=0.7).numpy()
+    tt = t(tgt2) / 255.0
+    mk["target_prep_64x48"] = torch.nn.functional.interpolate(
+        tt.permute(2, 0, 1).unsqueeze(0), size=(64, 48), mode="bilinear",
+        align_corners=False)[0].permute(1, 2, 0).contiguous().numpy()
+    mk["target_prep_150x90"] = torch.nn.functional.interpolate(
+        tt.permute(2, 0, 1).unsqueeze(0), size=(150, 90), mode="bilinear",
+        align_corners=False)[0].permute(1, 2, 0).contiguous().numpy()
     np.savez_compressed(os.path.join(HERE, "mask.npz"), **mk)
 
     with open(os.path.join(HERE, "meta.json"), "w") as fh:

@@ -81,7 +81,7 @@ def test_no_device_is_an_assertion_like_the_reference():
 
 
 # reference signatures (modules/render.py:204-214, fitness.py:8-12, fitness.py:35-39,
-# encode.py:4, :28, :63) — the drop-ins must accept the same parameters
+# encode.py:4, :28, :63, mask.py:29-38) — the drop-ins must accept the same parameters
 REF_SIGS = {
     ("render", "render_splats_rgb_triton"):
         ["genomes", "H", "W", "*k_sigma=3.0", "*device=None", "*background=(1.0, 1.0, 1.0)",
@@ -95,6 +95,9 @@ REF_SIGS = {
     ("encode", "axes_angle_to_cholesky"): ["a_log", "b_log", "theta"],
     ("encode", "genome_to_renderer"): ["ind_axes_angle"],
     ("encode", "genome_to_renderer_batched"): ["G_axes"],
+    ("mask", "compute_importance_mask"):
+        ["target_hw3", "H", "W", "edge_scales=(1, 2, 4)", "w_edge=0.7", "w_var=0.3", "gamma=0.7",
+         "floor=0.15", "smooth=0", "strength=1.0"],
 }
 
 
