@@ -81,7 +81,8 @@ def test_no_device_is_an_assertion_like_the_reference():
 
 
 # reference signatures (modules/render.py:204-214, fitness.py:8-12, fitness.py:35-39,
-# encode.py:4, :28, :63, mask.py:29-38) — the drop-ins must accept the same parameters
+# encode.py:4, :28, :63, mask.py:29-38, algorithm.py:17-31) — the drop-ins must accept the
+# same parameters (genetic_approx adds keyword-only **hooks: seed, draws, evaluate, ...)
 REF_SIGS = {
     ("render", "render_splats_rgb_triton"):
         ["genomes", "H", "W", "*k_sigma=3.0", "*device=None", "*background=(1.0, 1.0, 1.0)",
@@ -95,6 +96,12 @@ REF_SIGS = {
     ("encode", "axes_angle_to_cholesky"): ["a_log", "b_log", "theta"],
     ("encode", "genome_to_renderer"): ["ind_axes_angle"],
     ("encode", "genome_to_renderer_batched"): ["G_axes"],
+    ("algorithm", "genetic_approx"):
+        ["target_img_uint8", "H", "W", "device", "pop_size", "n_splats", "generations", "tour_k",
+         "elite_k", "cxpb", "mutpb", "mut_sigma_max", "mut_sigma_min", "schedule",
+         "min_scale_splats", "max_scale_splats", "k_sigma", "mask_strength", "boost_only",
+         "save_video=False", "frame_every=5000", "video_dir=''", "prefix='ga'",
+         "loss_png_path=''", "loss_csv_path=''", "loss_log_y=False", "hooks"],
     ("mask", "compute_importance_mask"):
         ["target_hw3", "H", "W", "edge_scales=(1, 2, 4)", "w_edge=0.7", "w_var=0.3", "gamma=0.7",
          "floor=0.15", "smooth=0", "strength=1.0"],

@@ -305,3 +305,43 @@ def test_drop_in_modules_numpy_and_torch():
     assert isinstance(img, torch.Tensor) and img.shape == (len(pop), H, W, 3)
     with pytest.raises(AssertionError):
         render_splats_rgb_triton(g9, H, W, device="cpu")
+
+
+# ---- GA layer on the GPU evaluator (§8f next #1) ----------------------------------------------
+def test_ga_reference_populations_fitness_on_gpu():
+    """Every population the reference's genetic_approx evaluated (recorded in
+    tests/golden/ga_loop.npz) gets the same fitness from libggs (rel 1e-5), with
+    the target prep and importance mask computed by ggs.mask."""
+    from ggs.mask import compute_importance_mask, prepare_target
+    d = load_golden("ga_loop.npz")
+    H, W = int(d["cfg"][0]), int(d["cfg"][1])
+    t = prepare_target(d["target"], H, W)
+    m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
+    for i in range(int(d["n_calls"])):
+        got = ggs.fitness(d[f"call{i}__pop"], t, H, W, 3.0, weight_mask=m)
+        np.testing.assert_allclose(got, d[f"call{i}__fit"], rtol=FIT_RTOL, err_msg=f"call {i}")
+
+
+def test_ga_end_to_end_on_gpu():
+    from modules.algorithm import genetic_approx
+    from ggs import ga
+    H = W = 64
+    target = np.random.default_rng(4).uniform(0, 255, (80, 72, 3)).astype(np.float32)
+    cfg = dict(mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0,
+                              "alpha": 25.0},
+               mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0,
+                              "alpha": 2.0}, schedule="cosine")
+    best, best_fit, st = ga.genetic_approx(
+        target, H, W, "cuda", pop_size=32, n_splats=48, generations=20, tour_k=2, elite_k=8,
+        cxpb=0.05, mutpb=0.05, min_scale_splats=3.0, max_scale_splats=0.1, k_sigma=3.0,
+        mask_strength=0.7, boost_only=False, seed=1, progress=False, return_state=True, **cfg)
+    c = st["curves"]["best"]
+    assert all(b <= a for a, b in zip(c, c[1:])) and c[-1] < c[0]
+    from ggs.mask import compute_importance_mask, prepare_target
+    t = prepare_target(target, H, W)
+    m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
+    assert float(ggs.fitness(best[None], t, H, W, 3.0, weight_mask=m)[0]) == best_fit
+    b2, f2 = genetic_approx(target, H, W, "cuda", 8, 16, 2, 2, 2, 0.05, 0.05, cfg["mut_sigma_max"],
+                            cfg["mut_sigma_min"], "cosine", 3.0, 0.1, 3.0, 0.7, False, seed=3,
+                            progress=False)
+    assert b2.shape == (16, 9) and np.isfinite(f2)

@@ -1,0 +1,50 @@
+"""GA layer throughput: generations/s of ggs.ga.genetic_approx at the bench
+workload (512x512, 256 splats, pop 128) — host-side batched operators + one
+libggs launch per generation — with the host/device split.
+
+usage: python tools/bench_ga.py [--gens 200] [--pop 128] [--splats 256] [--size 512]"""
+import argparse, json, os, sys, time
+import numpy as np
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "genetic-gaussian-splats_amd"))
+import ggs
+from ggs import ga
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--gens", type=int, default=200)
+ap.add_argument("--pop", type=int, default=128)
+ap.add_argument("--splats", type=int, default=256)
+ap.add_argument("--size", type=int, default=512)
+a = ap.parse_args()
+H = W = a.size
+target = np.random.default_rng(0).uniform(0, 255, (H, W, 3)).astype(np.float32)
+cfg = dict(mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0, "alpha": 25.0},
+           mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0, "alpha": 2.0},
+           schedule="cosine")
+t_eval = [0.0]
+from ggs.mask import compute_importance_mask, prepare_target
+t = prepare_target(target, H, W)
+m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
+
+def evaluate(G):
+    t0 = time.perf_counter()
+    f = ggs.fitness(G, t, H, W, 3.0, weight_mask=m)
+    t_eval[0] += time.perf_counter() - t0
+    return f
+
+ga.genetic_approx(target, H, W, "cuda", a.pop, a.splats, 3, 2, 8, 0.05, 0.05, min_scale_splats=3.0,
+                  max_scale_splats=0.1, k_sigma=3.0, mask_strength=0.7, boost_only=False, seed=0,
+                  evaluate=evaluate, progress=False, **cfg)          # warm-up
+t_eval[0] = 0.0
+t0 = time.perf_counter()
+best, fit = ga.genetic_approx(target, H, W, "cuda", a.pop, a.splats, a.gens, 2, 8, 0.05, 0.05,
+                              min_scale_splats=3.0, max_scale_splats=0.1, k_sigma=3.0,
+                              mask_strength=0.7, boost_only=False, seed=1, evaluate=evaluate,
+                              progress=False, **cfg)
+dt = time.perf_counter() - t0
+print(json.dumps({"metric": "GA generations/s", "value": round(a.gens / dt, 2),
+                  "config": {"H": H, "W": W, "splats": a.splats, "pop": a.pop, "gens": a.gens},
+                  "ms_per_gen": round(dt / a.gens * 1e3, 3),
+                  "eval_ms_per_gen (host API incl. copies)": round(t_eval[0] / a.gens * 1e3, 3),
+                  "host_ops_ms_per_gen": round((dt - t_eval[0]) / a.gens * 1e3, 3),
+                  "best_fit": fit}))
