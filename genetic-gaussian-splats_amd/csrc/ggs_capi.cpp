@@ -7,6 +7,7 @@
 //   fitness_many              modules/fitness.py:7-31    -> ggs_fitness / ggs_fitness_device
 //   (fitness_population fitness.py:34-47 and the list/tensor plumbing stay in Python)
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -658,6 +659,253 @@ void ggs_profile_reset(void) {
         g_prof_ms[k] = 0;
         g_prof_n[k] = 0;
     }
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// device-resident GA session (ggs_ga_*; kernels in ggs_ga.hip)
+// ---------------------------------------------------------------------------
+namespace ggs {
+namespace {
+
+struct GaSession {
+    DevCtx* c = nullptr;
+    hipStream_t st = nullptr;
+    ggs_ga_config cfg{};
+    int P = 0, N = 0, cur = 0;
+    DevBuf pop[2], fits[2], off, off_fits, src, target, mask, best_ind, best_fit, best_src,
+        best_upd, curves, draws;
+    int64_t n_curves = 0, curves_cap = 0;
+};
+
+double anneal_factor(int gen, int total, int kind) {          // utils.py:14-27
+    const int g = std::max(0, std::min(gen, total));
+    const double p = (double)g / (double)std::max(1, total);
+    double raw;
+    if (kind == 1) raw = 0.5 * (1.0 + cos(M_PI * p));
+    else if (kind == 2) raw = pow(pow(0.2, 1.0 / (double)std::max(1, total)), (double)g);
+    else raw = 1.0 - p;
+    return std::max(0.0, raw);
+}
+
+GaParamsDev ga_params(const ggs_ga_config& c, int gen, int total) {   // build_mut_sigma
+    const double f = anneal_factor(gen, total, c.schedule);
+    float sig[6];
+    for (int k = 0; k < 6; ++k)
+        sig[k] = (float)(c.sig_min[k] + f * (c.sig_max[k] - c.sig_min[k]));
+    GaParamsDev p;
+    p.sig_xy = sig[0]; p.sig_alog = sig[1]; p.sig_blog = sig[2]; p.sig_theta = sig[3];
+    p.sig_rgb = sig[4]; p.sig_alpha = sig[5];
+    p.mutpb = c.mutpb; p.cxpb = c.cxpb; p.tour_k = c.tour_k;
+    p.log_lo = c.scale_log_lo; p.log_hi = c.scale_log_hi;
+    return p;
+}
+
+GaBestDev ga_best(GaSession* s) {
+    return {(double*)s->best_fit.p, (int*)s->best_src.p, (int*)s->best_upd.p, (float*)s->best_ind.p};
+}
+
+int ga_curves_row(GaSession* s, double** row) {
+    if (s->n_curves >= s->curves_cap) {
+        const int64_t cap = std::max<int64_t>(64, s->curves_cap * 2);
+        DevBuf nb;
+        GGS_HIP(hipMalloc(&nb.p, sizeof(double) * 3 * cap));
+        nb.cap = sizeof(double) * 3 * cap;
+        if (s->curves.p) {
+            GGS_HIP(hipMemcpyAsync(nb.p, s->curves.p, sizeof(double) * 3 * s->n_curves,
+                                   hipMemcpyDeviceToDevice, s->st));
+            GGS_HIP(hipStreamSynchronize(s->st));
+            GGS_HIP(hipFree(s->curves.p));
+        }
+        s->curves = nb;
+        s->curves_cap = cap;
+    }
+    *row = (double*)s->curves.p + 3 * s->n_curves;
+    return GGS_OK;
+}
+
+// Upload one generation's explicit draws into s->draws; returns device views.
+int ga_upload_draws(GaSession* s, const ggs_ga_draws* h, GaDrawsDev* d) {
+    const int64_t P = s->P, N = s->N, K = s->cfg.tour_k, np2 = (P + 1) / 2;
+    struct Seg { const void* src; int64_t bytes; const void** dst; };
+    Seg segs[] = {
+        {h->tour_idx, 4 * P * K, (const void**)&d->tour_idx}, {h->perm, 4 * P, (const void**)&d->perm},
+        {h->cx, 4 * np2, (const void**)&d->cx}, {h->cx_u, 4 * np2 * N, (const void**)&d->cx_u},
+        {h->u_xy, 8 * P * N, (const void**)&d->u_xy}, {h->u_ab, 8 * P * N, (const void**)&d->u_ab},
+        {h->u_t, 4 * P * N, (const void**)&d->u_t}, {h->u_rgb, 4 * P * N, (const void**)&d->u_rgb},
+        {h->u_a, 4 * P * N, (const void**)&d->u_a}, {h->k_color, 4 * P, (const void**)&d->k_color},
+        {h->k_xy, 4 * P, (const void**)&d->k_xy}, {h->k_ab, 4 * P, (const void**)&d->k_ab},
+        {h->k_t, 4 * P, (const void**)&d->k_t}, {h->n_xy, 8 * P * N, (const void**)&d->n_xy},
+        {h->n_ab, 8 * P * N, (const void**)&d->n_ab}, {h->n_t, 4 * P * N, (const void**)&d->n_t},
+        {h->n_rgba, 16 * P * N, (const void**)&d->n_rgba}, {h->swap_i, 4 * P, (const void**)&d->swap_i},
+        {h->swap_pick, 4 * P, (const void**)&d->swap_pick}, {h->swap_u, 8 * P, (const void**)&d->swap_u},
+    };
+    int64_t total = 0;
+    for (const Seg& g : segs) {
+        if (!g.src) return fail(GGS_EINVAL, "ggs_ga_step: every draws array is required");
+        total += (g.bytes + 255) & ~(int64_t)255;
+    }
+    int rc;
+    if ((rc = ensure(s->draws, (size_t)total, s->st))) return rc;
+    GGS_HIP(hipStreamSynchronize(s->st));   // previous generation may still read the buffer
+    char* base = (char*)s->draws.p;
+    for (const Seg& g : segs) {
+        GGS_HIP(hipMemcpyAsync(base, g.src, (size_t)g.bytes, hipMemcpyHostToDevice, s->st));
+        *g.dst = base;
+        base += (g.bytes + 255) & ~(int64_t)255;
+    }
+    return GGS_OK;
+}
+
+int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
+    GaDrawsDev d{};
+    int rc;
+    if (hd && (rc = ga_upload_draws(s, hd, &d))) return rc;
+    const int P = s->P, N = s->N, nxt = 1 - s->cur;
+    const GaParamsDev prm = ga_params(s->cfg, gen, total);
+    GGS_HIP(launch_ga_variation(s->st, (const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
+                                P, N, prm, d, s->cfg.seed, gen, (float*)s->off.p));
+    if ((rc = run_fitness(s->c, s->st, (const float*)s->off.p, P, N, 9, (const float*)s->target.p,
+                          s->mask.p ? (const float*)s->mask.p : nullptr, s->cfg.fitness_mode,
+                          s->cfg.boost_beta, s->cfg.H, s->cfg.W, s->cfg.k_sigma, (float*)s->off_fits.p)))
+        return rc;
+    double* row;
+    if ((rc = ga_curves_row(s, &row))) return rc;
+    GGS_HIP(launch_ga_survivors(s->st, (const float*)s->fits[s->cur].p, (const float*)s->off_fits.p, P,
+                                s->cfg.elite_k, (int*)s->src.p, (float*)s->fits[nxt].p, ga_best(s), row, 0));
+    GGS_HIP(launch_ga_gather(s->st, (const float*)s->pop[s->cur].p, (const float*)s->off.p, P, N,
+                             (const int*)s->src.p, (float*)s->pop[nxt].p, ga_best(s), 0));
+    s->cur = nxt;
+    s->n_curves += 1;
+    return GGS_OK;
+}
+
+void ga_free(GaSession* s) {
+    for (DevBuf* b : {&s->pop[0], &s->pop[1], &s->fits[0], &s->fits[1], &s->off, &s->off_fits, &s->src,
+                      &s->target, &s->mask, &s->best_ind, &s->best_fit, &s->best_src, &s->best_upd,
+                      &s->curves, &s->draws})
+        if (b->p) (void)hipFree(b->p);
+    if (s->st) (void)hipStreamDestroy(s->st);
+}
+
+}  // namespace
+}  // namespace ggs
+
+extern "C" {
+
+int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_hw3,
+                  const float* mask_hw, const float* init_pop, void** handle) {
+    if (!cfg || !target_hw3 || !init_pop || !handle) return fail(GGS_EINVAL, "null argument");
+    const ggs_ga_config& c = *cfg;
+    int rc = check_dims(c.pop_size, c.n_splats, 9, c.H, c.W);
+    if (rc) return rc;
+    if (c.pop_size < 1 || c.pop_size > ga_max_population())
+        return fail(GGS_EINVAL, "pop_size must be in [1, %d]", ga_max_population());
+    if (c.tour_k < 1) return fail(GGS_EINVAL, "tour_k must be >= 1");
+    if (c.elite_k > c.pop_size) return fail(GGS_EINVAL, "elite_k must be <= pop_size");
+    if (c.fitness_mode < GGS_FIT_NONE || c.fitness_mode > GGS_FIT_BOOST)
+        return fail(GGS_EINVAL, "bad fitness mode %d", c.fitness_mode);
+    if (c.fitness_mode != GGS_FIT_NONE && !mask_hw) return fail(GGS_EINVAL, "mode needs a mask");
+    DevCtx* ctx = nullptr;
+    if ((rc = get_ctx(device, &ctx))) return rc;
+    auto s = std::make_unique<GaSession>();
+    s->c = ctx;
+    s->cfg = c;
+    if (s->cfg.scale_log_lo == 0.0f && s->cfg.scale_log_hi == 0.0f) {
+        s->cfg.scale_log_lo = logf(c.min_scale_splats);
+        s->cfg.scale_log_hi = logf(c.max_scale_splats * (float)std::max(c.H, c.W));
+    }
+    s->P = c.pop_size;
+    s->N = c.n_splats;
+    const size_t pb = sizeof(float) * 9 * (size_t)s->P * s->N, hw = (size_t)c.H * c.W;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard dg(ctx->dev);
+    auto bail = [&](int code) { ga_free(s.get()); return code; };
+    if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(GGS_EHIP, "stream creation failed"));
+    for (DevBuf* b : {&s->pop[0], &s->pop[1], &s->off})
+        if ((rc = ensure(*b, std::max<size_t>(pb, 4), s->st))) return bail(rc);
+    for (DevBuf* b : {&s->fits[0], &s->fits[1], &s->off_fits})
+        if ((rc = ensure(*b, sizeof(float) * s->P, s->st))) return bail(rc);
+    if ((rc = ensure(s->src, sizeof(int) * s->P, s->st))) return bail(rc);
+    if ((rc = ensure(s->target, sizeof(float) * 3 * hw, s->st))) return bail(rc);
+    if (mask_hw && (rc = ensure(s->mask, sizeof(float) * hw, s->st))) return bail(rc);
+    if ((rc = ensure(s->best_ind, std::max<size_t>(sizeof(float) * 9 * s->N, 4), s->st))) return bail(rc);
+    if ((rc = ensure(s->best_fit, sizeof(double), s->st))) return bail(rc);
+    if ((rc = ensure(s->best_src, sizeof(int), s->st))) return bail(rc);
+    if ((rc = ensure(s->best_upd, sizeof(int), s->st))) return bail(rc);
+    if (hipMemcpyAsync(s->target.p, target_hw3, sizeof(float) * 3 * hw, hipMemcpyHostToDevice, s->st) ||
+        (mask_hw && hipMemcpyAsync(s->mask.p, mask_hw, sizeof(float) * hw, hipMemcpyHostToDevice, s->st)) ||
+        hipMemcpyAsync(s->pop[0].p, init_pop, pb, hipMemcpyHostToDevice, s->st))
+        return bail(fail(GGS_EHIP, "upload failed"));
+    if ((rc = run_fitness(ctx, s->st, (const float*)s->pop[0].p, s->P, s->N, 9, (const float*)s->target.p,
+                          mask_hw ? (const float*)s->mask.p : nullptr, c.fitness_mode, c.boost_beta,
+                          c.H, c.W, c.k_sigma, (float*)s->fits[0].p)))
+        return bail(rc);
+    double* row;
+    if ((rc = ga_curves_row(s.get(), &row))) return bail(rc);
+    if (launch_ga_survivors(s->st, (const float*)s->fits[0].p, nullptr, s->P, c.elite_k, (int*)s->src.p,
+                            nullptr, ga_best(s.get()), row, 1) ||
+        launch_ga_gather(s->st, (const float*)s->pop[0].p, nullptr, s->P, s->N, nullptr, nullptr,
+                         ga_best(s.get()), 1))
+        return bail(fail(GGS_EHIP, "init launch failed"));
+    if (hipStreamSynchronize(s->st) != hipSuccess)     // init_pop / target may be freed on return
+        return bail(fail(GGS_EHIP, "initial evaluation failed"));
+    s->n_curves = 1;
+    *handle = s.release();
+    return GGS_OK;
+}
+
+int ggs_ga_step(void* handle, int32_t gen, int32_t total_gens, const ggs_ga_draws* draws) {
+    if (!handle) return fail(GGS_EINVAL, "null handle");
+    GaSession* s = (GaSession*)handle;
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    DeviceGuard dg(s->c->dev);
+    const int rc = ga_generation(s, gen, total_gens, draws);
+    if (rc || !draws) return rc;
+    GGS_HIP(hipStreamSynchronize(s->st));   // the caller's draw arrays are released on return
+    return GGS_OK;
+}
+
+int ggs_ga_run(void* handle, int32_t first_gen, int32_t n_gens, int32_t total_gens) {
+    if (!handle || n_gens < 0) return fail(GGS_EINVAL, "bad arguments");
+    GaSession* s = (GaSession*)handle;
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    DeviceGuard dg(s->c->dev);
+    for (int g = 0; g < n_gens; ++g) {
+        const int rc = ga_generation(s, first_gen + g, total_gens, nullptr);
+        if (rc) return rc;
+    }
+    return GGS_OK;
+}
+
+int ggs_ga_read(void* handle, float* pop, float* fits, float* best_ind, double* best_fit,
+                double* curves, int32_t* n_curves) {
+    if (!handle) return fail(GGS_EINVAL, "null handle");
+    GaSession* s = (GaSession*)handle;
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    DeviceGuard dg(s->c->dev);
+    GGS_HIP(hipStreamSynchronize(s->st));
+    if (pop) GGS_HIP(hipMemcpy(pop, s->pop[s->cur].p, sizeof(float) * 9 * (size_t)s->P * s->N, hipMemcpyDeviceToHost));
+    if (fits) GGS_HIP(hipMemcpy(fits, s->fits[s->cur].p, sizeof(float) * s->P, hipMemcpyDeviceToHost));
+    if (best_ind) GGS_HIP(hipMemcpy(best_ind, s->best_ind.p, sizeof(float) * 9 * (size_t)s->N, hipMemcpyDeviceToHost));
+    if (best_fit) GGS_HIP(hipMemcpy(best_fit, s->best_fit.p, sizeof(double), hipMemcpyDeviceToHost));
+    if (curves) GGS_HIP(hipMemcpy(curves, s->curves.p, sizeof(double) * 3 * s->n_curves, hipMemcpyDeviceToHost));
+    if (n_curves) *n_curves = (int32_t)s->n_curves;
+    return GGS_OK;
+}
+
+void ggs_ga_destroy(void* handle) {
+    if (!handle) return;
+    GaSession* s = (GaSession*)handle;
+    {
+        std::lock_guard<std::mutex> lk(s->c->mu);
+        DeviceGuard dg(s->c->dev);
+        if (s->st) (void)hipStreamSynchronize(s->st);
+        ga_free(s);
+    }
+    delete s;
 }
 
 }  // extern "C"

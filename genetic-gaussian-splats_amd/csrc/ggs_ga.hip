@@ -1,0 +1,420 @@
+// Device-resident genetic algorithm around the fitness pipeline (SURVEY.md §8f
+// next #1: algorithm.py:85-141, genetic.py:8-91, utils.py:10-45 on the GPU).
+//
+// Per generation (all on one stream, no host round trip):
+//   variation  1 workgroup / offspring: tournament (genetic.py:8-14), uniform
+//              row crossover (:17-21), masked Gaussian mutation with the >=1-flag
+//              guarantees (:32-77), wrap/clamp (utils.py:35-45), size-ordered
+//              splat swap (:79-91).  Same float32 operation order as ggs/ga.py,
+//              which is replay-verified against the reference.
+//   fitness    prep + raster + finalize (ggs_kernels.hip) on the offspring
+//   survivors  1 workgroup: stable sort of the parents' fitness -> elites,
+//              next population = elites + offspring[:P-E] (algorithm.py:129-141),
+//              best-so-far (:144-150) and the curves (:153-155)
+//   gather     1 workgroup / individual: builds the next population buffer
+// Draws come either from explicit per-generation arrays (replay / parity with the
+// host path) or from a counter-based Philox4x32-10 generator keyed by
+// (seed, generation, individual, splat), which needs no state between launches.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ggs_internal.h"
+
+namespace ggs {
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11), counter-based
+// ---------------------------------------------------------------------------
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        c = {(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
+
+// stream ids: which draw a 4-word Philox block feeds
+enum : uint32_t { S_MASK = 1, S_NORM_A = 2, S_NORM_B = 3, S_NORM_C = 4, S_IND = 5, S_TOUR = 6, S_CX = 7 };
+
+struct Rng {
+    uint32_t k0, k1, gen;
+    __device__ U4 block(uint32_t stream, uint32_t who, uint32_t what) const {
+        return philox({gen, who, what, stream}, k0, k1);
+    }
+};
+
+__device__ __forceinline__ float normal_from(uint32_t a, uint32_t b) {   // Box-Muller
+    const float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);      // (0, 1]
+    const float u2 = u01(b);
+    return sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
+}
+
+// ---------------------------------------------------------------------------
+// float32 helpers with ggs/ga.py's exact semantics
+// ---------------------------------------------------------------------------
+constexpr float PI32 = 3.14159274101257324219f;     // float32(pi)
+constexpr float TWO_PI32 = 6.28318548202514648438f; // float32(2*pi)
+
+__device__ __forceinline__ float wrap_angle(float th) {      // np.remainder(th + pi, 2pi) - pi
+    const float x = th + PI32;
+    float r = fmodf(x, TWO_PI32);
+    if (r != 0.0f && (r < 0.0f) != (TWO_PI32 < 0.0f)) r += TWO_PI32;
+    return r - PI32;
+}
+__device__ __forceinline__ float clip(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+// ---------------------------------------------------------------------------
+// variation
+// ---------------------------------------------------------------------------
+__device__ int tournament_pick(const float* __restrict__ fits, const GaDrawsDev& d, const Rng& rng,
+                               int q, int P, int k) {
+    int best = -1;
+    for (int j = 0; j < k; ++j) {
+        int i;
+        if (d.tour_idx) {
+            i = d.tour_idx[q * k + j];
+        } else {
+            const U4 r = rng.block(S_TOUR, (uint32_t)q, (uint32_t)j);
+            i = min((int)(u01(r.x) * (float)P), P - 1);
+        }
+        if (best < 0 || fits[i] < fits[best]) best = i;        // genetic.py:11-13: strict <
+    }
+    return best;
+}
+
+constexpr int VT = 256;   // threads per variation workgroup
+
+__global__ void __launch_bounds__(VT)
+ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fits, int P, int N,
+                    GaParamsDev prm, GaDrawsDev d, uint32_t k0, uint32_t k1, int gen,
+                    float* __restrict__ off) {
+    __shared__ int s_a, s_b, s_cx;
+    __shared__ float s_sizei;
+    __shared__ int s_j, s_count;
+    __shared__ int s_scan[VT / 64];
+    const int o = blockIdx.x;                  // offspring index
+    const int pair = o >> 1;
+    const bool first = (o & 1) == 0;
+    const int tid = threadIdx.x;
+    const Rng rng{k0, k1, (uint32_t)gen};
+
+    if (tid == 0) {
+        // parents 2*pair and 2*pair+1 of the (shuffled) tournament winners
+        const int qa = d.perm ? d.perm[2 * pair] : 2 * pair;
+        const int qb = d.perm ? d.perm[(2 * pair + 1) % P] : (2 * pair + 1) % P;
+        s_a = tournament_pick(fits, d, rng, qa, P, prm.tour_k);
+        s_b = tournament_pick(fits, d, rng, qb, P, prm.tour_k);
+        if (d.cx) s_cx = d.cx[pair];
+        else s_cx = u01(rng.block(S_CX, (uint32_t)pair, 0).x) < prm.cxpb;
+    }
+    __syncthreads();
+    const float* __restrict__ A = pop + (int64_t)s_a * N * 9;
+    const float* __restrict__ Bp = pop + (int64_t)s_b * N * 9;
+    float* __restrict__ O = off + (int64_t)o * N * 9;
+    const float p = prm.mutpb;
+    const int64_t ob = (int64_t)o * N;
+
+    // pass 1: crossover + mask flags, any() per mask group
+    int any_color = 0, any_xy = 0, any_ab = 0, any_t = 0;
+    for (int s = tid; s < N; s += VT) {
+        float ux0, ux1, ua0, ua1, ut, urgb, ua;
+        if (d.u_xy) {
+            ux0 = d.u_xy[(ob + s) * 2]; ux1 = d.u_xy[(ob + s) * 2 + 1];
+            ua0 = d.u_ab[(ob + s) * 2]; ua1 = d.u_ab[(ob + s) * 2 + 1];
+            ut = d.u_t[ob + s]; urgb = d.u_rgb[ob + s]; ua = d.u_a[ob + s];
+        } else {
+            const U4 r1 = rng.block(S_MASK, (uint32_t)o, (uint32_t)(2 * s));
+            const U4 r2 = rng.block(S_MASK, (uint32_t)o, (uint32_t)(2 * s + 1));
+            ux0 = u01(r1.x); ux1 = u01(r1.y); ua0 = u01(r1.z); ua1 = u01(r1.w);
+            ut = u01(r2.x); urgb = u01(r2.y); ua = u01(r2.z);
+        }
+        any_color |= (urgb < p) | (ua < p);
+        any_xy |= (ux0 < p) | (ux1 < p);
+        any_ab |= (ua0 < p) | (ua1 < p);
+        any_t |= (ut < p);
+    }
+    any_color = __syncthreads_or(any_color);
+    any_xy = __syncthreads_or(any_xy);
+    any_ab = __syncthreads_or(any_ab);
+    any_t = __syncthreads_or(any_t);
+    // genetic.py:24-29: fallback flat indices (k into [N,2] or [N,1] row-major)
+    int kc = -1, kx = -1, kb = -1, kt = -1;
+    if (!any_color) kc = d.k_color ? d.k_color[o] : (int)(rng.block(S_IND, (uint32_t)o, 0).x % (uint32_t)(2 * N));
+    if (!any_xy) kx = d.k_xy ? d.k_xy[o] : (int)(rng.block(S_IND, (uint32_t)o, 1).x % (uint32_t)(2 * N));
+    if (!any_ab) kb = d.k_ab ? d.k_ab[o] : (int)(rng.block(S_IND, (uint32_t)o, 2).x % (uint32_t)(2 * N));
+    if (!any_t) kt = d.k_t ? d.k_t[o] : (int)(rng.block(S_IND, (uint32_t)o, 3).x % (uint32_t)N);
+
+    // pass 2: build the child row, mutate, wrap, clamp -> off
+    for (int s = tid; s < N; s += VT) {
+        float ux0, ux1, ua0, ua1, ut, urgb, ua, cxu = 0.0f;
+        float nx0, nx1, na0, na1, nt, nr0, nr1, nr2, nr3;
+        if (d.u_xy) {
+            ux0 = d.u_xy[(ob + s) * 2]; ux1 = d.u_xy[(ob + s) * 2 + 1];
+            ua0 = d.u_ab[(ob + s) * 2]; ua1 = d.u_ab[(ob + s) * 2 + 1];
+            ut = d.u_t[ob + s]; urgb = d.u_rgb[ob + s]; ua = d.u_a[ob + s];
+            nx0 = d.n_xy[(ob + s) * 2]; nx1 = d.n_xy[(ob + s) * 2 + 1];
+            na0 = d.n_ab[(ob + s) * 2]; na1 = d.n_ab[(ob + s) * 2 + 1];
+            nt = d.n_t[ob + s];
+            nr0 = d.n_rgba[(ob + s) * 4]; nr1 = d.n_rgba[(ob + s) * 4 + 1];
+            nr2 = d.n_rgba[(ob + s) * 4 + 2]; nr3 = d.n_rgba[(ob + s) * 4 + 3];
+            if (s_cx) cxu = d.cx_u[(int64_t)pair * N + s];
+        } else {
+            const U4 r1 = rng.block(S_MASK, (uint32_t)o, (uint32_t)(2 * s));
+            const U4 r2 = rng.block(S_MASK, (uint32_t)o, (uint32_t)(2 * s + 1));
+            ux0 = u01(r1.x); ux1 = u01(r1.y); ua0 = u01(r1.z); ua1 = u01(r1.w);
+            ut = u01(r2.x); urgb = u01(r2.y); ua = u01(r2.z);
+            const U4 g1 = rng.block(S_NORM_A, (uint32_t)o, (uint32_t)s);
+            const U4 g2 = rng.block(S_NORM_B, (uint32_t)o, (uint32_t)s);
+            const U4 g3 = rng.block(S_NORM_C, (uint32_t)o, (uint32_t)s);
+            nx0 = normal_from(g1.x, g1.y); nx1 = normal_from(g1.z, g1.w);
+            na0 = normal_from(g2.x, g2.y); na1 = normal_from(g2.z, g2.w);
+            nt = normal_from(g3.x, g3.y); nr0 = normal_from(g3.z, g3.w);
+            const U4 g4 = rng.block(S_NORM_C, (uint32_t)o, (uint32_t)(s + N));
+            nr1 = normal_from(g4.x, g4.y); nr2 = normal_from(g4.z, g4.w);
+            const U4 g5 = rng.block(S_NORM_C, (uint32_t)o, (uint32_t)(s + 2 * N));
+            nr3 = normal_from(g5.x, g5.y);
+            if (s_cx) cxu = u01(rng.block(S_CX, (uint32_t)pair, (uint32_t)(s + 1)).x);   // shared by the pair
+        }
+        // genetic.py:17-21 (c1 = where(m, a, b), c2 = where(m, b, a)) / duplicate
+        const bool m = cxu < 0.5f;
+        const bool takeA = s_cx ? (first ? m : !m) : first;
+        const float* src = (takeA ? A : Bp) + (int64_t)s * 9;
+        float g[9];
+#pragma unroll
+        for (int c = 0; c < 9; ++c) g[c] = src[c];
+        // flags (genetic.py:37-54) with the one-true fallbacks
+        const bool mrgb = (urgb < p) || (kc == 2 * s), ma = (ua < p) || (kc == 2 * s + 1);
+        const bool mx0 = (ux0 < p) || (kx == 2 * s), mx1 = (ux1 < p) || (kx == 2 * s + 1);
+        const bool mb0 = (ua0 < p) || (kb == 2 * s), mb1 = (ua1 < p) || (kb == 2 * s + 1);
+        const bool mt = (ut < p) || (kt == s);
+        // genetic.py:57-70, same float32 op order as ggs/ga.py
+        g[0] = g[0] + (nx0 * prm.sig_xy) * (float)mx0;
+        g[1] = g[1] + (nx1 * prm.sig_xy) * (float)mx1;
+        g[2] = g[2] + (na0 * prm.sig_alog) * (float)mb0;
+        g[3] = g[3] + (na1 * prm.sig_blog) * (float)mb1;
+        g[4] = g[4] + (nt * prm.sig_theta) * (float)mt;
+        g[4] = wrap_angle(g[4]);
+        g[5] = g[5] + (nr0 * prm.sig_rgb) * (float)mrgb;
+        g[6] = g[6] + (nr1 * prm.sig_rgb) * (float)mrgb;
+        g[7] = g[7] + (nr2 * prm.sig_rgb) * (float)mrgb;
+        g[8] = g[8] + (nr3 * prm.sig_alpha) * (float)ma;
+        // clamp_genome (utils.py:35-45)
+        g[0] = clip(g[0], 0.0f, 1.0f);
+        g[1] = clip(g[1], 0.0f, 1.0f);
+        g[2] = clip(g[2], prm.log_lo, prm.log_hi);
+        g[3] = clip(g[3], prm.log_lo, prm.log_hi);
+        g[4] = wrap_angle(g[4]);
+#pragma unroll
+        for (int c = 5; c < 9; ++c) g[c] = clip(g[c], 0.0f, 255.0f);
+#pragma unroll
+        for (int c = 0; c < 9; ++c) O[(int64_t)s * 9 + c] = g[c];
+    }
+    if (N < 2) return;
+    __syncthreads();   // workgroup-scope ordering of the rows just written
+
+    // genetic.py:79-91: pick i, then the pick-th later splat bigger than i
+    int i;
+    if (d.swap_i) i = d.swap_i[o];
+    else i = (int)(rng.block(S_IND, (uint32_t)o, 4).x % (uint32_t)(N - 1));
+    if (tid == 0) {
+        s_sizei = expf(O[(int64_t)i * 9 + 2]) * expf(O[(int64_t)i * 9 + 3]);
+        s_j = -1;
+    }
+    __syncthreads();
+    const float sizei = s_sizei;
+    int cnt = 0;
+    for (int s = tid; s < N; s += VT)
+        cnt += (s > i) && (expf(O[(int64_t)s * 9 + 2]) * expf(O[(int64_t)s * 9 + 3]) > sizei);
+    {   // total candidates: workgroup sum
+        const int lane = tid & 63, w = tid >> 6;
+        int v = cnt;
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) s_scan[w] = v;
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int k = 0; k < VT / 64; ++k) tot += s_scan[k];
+            s_count = tot;
+        }
+        __syncthreads();
+    }
+    const int count = s_count;
+    if (count == 0) return;
+    int pick;
+    if (d.swap_pick && d.swap_pick[o] >= 0) pick = d.swap_pick[o];
+    else {
+        const double u = d.swap_u ? d.swap_u[o] : (double)u01(rng.block(S_IND, (uint32_t)o, 5).x);
+        pick = (int)(u * (double)count);
+        if (pick > count - 1) pick = count - 1;
+    }
+    // find the (pick+1)-th candidate in splat order: walk 256-splat chunks
+    int seen = 0;
+    for (int base = 0; base < N; base += VT) {
+        const int s = base + tid;
+        const bool c = s < N && s > i &&
+                       (expf(O[(int64_t)s * 9 + 2]) * expf(O[(int64_t)s * 9 + 3]) > sizei);
+        // exclusive prefix of c across the workgroup (in s order)
+        const uint64_t bal = __ballot(c);
+        const int lane = tid & 63, w = tid >> 6;
+        const int inwave = __popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+        __syncthreads();
+        if (lane == 0) s_scan[w] = __popcll(bal);
+        __syncthreads();
+        int before = seen;
+        for (int k = 0; k < w; ++k) before += s_scan[k];
+        if (c && before + inwave == pick) s_j = s;
+        int tot = 0;
+        for (int k = 0; k < VT / 64; ++k) tot += s_scan[k];
+        seen += tot;
+        __syncthreads();
+        if (s_j >= 0) break;
+    }
+    const int j = s_j;
+    if (tid < 9 && j >= 0) {
+        const float a = O[(int64_t)i * 9 + tid], b = O[(int64_t)j * 9 + tid];
+        O[(int64_t)i * 9 + tid] = b;
+        O[(int64_t)j * 9 + tid] = a;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// survivors: elites by stable fitness order, next fitness vector, best, curves
+// ---------------------------------------------------------------------------
+constexpr int ST = 1024;   // one workgroup; bitonic sort of up to 4096 keys in LDS
+constexpr int SMAX = 4096;
+
+__global__ void __launch_bounds__(ST)
+ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ off_fits, int P,
+                    int elite_k, int* __restrict__ src, float* __restrict__ new_fits,
+                    GaBestDev best, double* __restrict__ curves_row, int init) {
+    __shared__ float key[SMAX];
+    __shared__ int idx[SMAX];
+    const int tid = threadIdx.x;
+    int n2 = 1;
+    while (n2 < P) n2 <<= 1;
+    if (!init) {
+        for (int i = tid; i < n2; i += ST) {
+            key[i] = i < P ? fits[i] : __builtin_inff();
+            idx[i] = i < P ? i : 0x7fffffff;
+        }
+        __syncthreads();
+        // bitonic sort on (key, idx): lexicographic == Python's stable sorted()
+        for (int k = 2; k <= n2; k <<= 1) {
+            for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                for (int i = tid; i < n2; i += ST) {
+                    const int l = i ^ jj;
+                    if (l > i) {
+                        const bool up = (i & k) == 0;
+                        const bool gt = key[i] > key[l] || (key[i] == key[l] && idx[i] > idx[l]);
+                        if (gt == up) {
+                            const float tk = key[i]; key[i] = key[l]; key[l] = tk;
+                            const int ti = idx[i]; idx[i] = idx[l]; idx[l] = ti;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        const int E = elite_k < 1 ? 1 : elite_k;                  // algorithm.py:129
+        for (int r = tid; r < P; r += ST) {
+            if (r < E) {
+                src[r] = idx[r];                                  // from the parents
+                new_fits[r] = fits[idx[r]];
+            } else {
+                src[r] = P + (r - E);                             // offspring r - E
+                new_fits[r] = off_fits[r - E];
+            }
+        }
+        __syncthreads();
+    }
+    const float* __restrict__ F = init ? fits : new_fits;
+    // best so far (algorithm.py:64-67, 143-150) and curves (:71-75, 153-155)
+    if (tid == 0) {
+        int g = 0;
+        for (int r = 1; r < P; ++r)
+            if (F[r] < F[g]) g = r;
+        const double fg = (double)F[g];
+        if (init || fg + 1e-10 < *best.fit) {
+            *best.fit = fg;
+            *best.src = init ? g : src[g];
+            *best.updated = 1;
+        } else {
+            *best.updated = 0;
+        }
+        double sum = 0.0;                                         // sum(fitnesses) / len
+        for (int r = 0; r < P; ++r) sum += (double)F[r];
+        curves_row[0] = *best.fit;
+        curves_row[1] = sum / (double)P;
+    }
+    // median: sort the new fitness values (statistics.median on the list)
+    for (int i = tid; i < n2; i += ST) key[i] = i < P ? F[i] : __builtin_inff();
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = tid; i < n2; i += ST) {
+                const int l = i ^ jj;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    if ((key[i] > key[l]) == up) {
+                        const float t = key[i]; key[i] = key[l]; key[l] = t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0)
+        curves_row[2] = (P & 1) ? (double)key[P / 2] : ((double)key[P / 2 - 1] + (double)key[P / 2]) / 2.0;
+}
+
+// next population rows from (parents | offspring) by src; best row if improved
+__global__ void __launch_bounds__(256)
+ga_gather_kernel(const float* __restrict__ pop, const float* __restrict__ off, int P, int N,
+                 const int* __restrict__ src, float* __restrict__ next, GaBestDev best, int init) {
+    const int r = blockIdx.x;
+    const int sidx = init ? r : src[r];
+    const float* from = sidx < P ? pop + (int64_t)sidx * N * 9 : off + (int64_t)(sidx - P) * N * 9;
+    float* to = next + (int64_t)r * N * 9;
+    const int64_t n = (int64_t)N * 9;
+    if (!init)
+        for (int64_t i = threadIdx.x; i < n; i += 256) to[i] = from[i];
+    if (*best.updated && *best.src == sidx)      // the new best individual
+        for (int64_t i = threadIdx.x; i < n; i += 256) best.ind[i] = from[i];
+}
+
+// ---------------------------------------------------------------------------
+hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
+                               const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
+                               float* off) {
+    hipLaunchKernelGGL(ga_variation_kernel, dim3(P), dim3(VT), 0, st, pop, fits, P, N, prm, d,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), gen, off);
+    return hipGetLastError();
+}
+
+hipError_t launch_ga_survivors(hipStream_t st, const float* fits, const float* off_fits, int P,
+                               int elite_k, int* src, float* new_fits, const GaBestDev& best,
+                               double* curves_row, int init) {
+    hipLaunchKernelGGL(ga_survivors_kernel, dim3(1), dim3(ST), 0, st, fits, off_fits, P, elite_k,
+                       src, new_fits, best, curves_row, init);
+    return hipGetLastError();
+}
+
+hipError_t launch_ga_gather(hipStream_t st, const float* pop, const float* off, int P, int N,
+                            const int* src, float* next, const GaBestDev& best, int init) {
+    hipLaunchKernelGGL(ga_gather_kernel, dim3(P), dim3(256), 0, st, pop, off, P, N, src, next, best,
+                       init);
+    return hipGetLastError();
+}
+
+int ga_max_population() { return SMAX; }
+
+}  // namespace ggs

@@ -35,4 +35,41 @@ hipError_t launch_detmath(hipStream_t st, const float* x, const float* y, int64_
 hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,
                            int nTiles, int mode, int H, int W, float* out);
 
+// ---- device GA (ggs_ga.hip) -------------------------------------------------
+struct GaParamsDev {            // one generation's operator parameters (float32 as the host path)
+    float sig_xy, sig_alog, sig_blog, sig_theta, sig_rgb, sig_alpha;   // build_mut_sigma
+    float mutpb, cxpb;
+    int tour_k;
+    float log_lo, log_hi;       // clamp_genome scale bounds (utils.py:38-39)
+};
+struct GaDrawsDev {             // explicit draws (device pointers); all NULL -> Philox in-kernel
+    const int* tour_idx;        // [P*k]
+    const int* perm;            // [P]
+    const int* cx;              // [npairs]
+    const float* cx_u;          // [npairs*N]
+    const float *u_xy, *u_ab;   // [P*N*2]
+    const float *u_t, *u_rgb, *u_a;   // [P*N]
+    const int *k_color, *k_xy, *k_ab, *k_t;   // [P]
+    const float *n_xy, *n_ab;   // [P*N*2]
+    const float* n_t;           // [P*N]
+    const float* n_rgba;        // [P*N*4]
+    const int *swap_i, *swap_pick;    // [P]
+    const double* swap_u;       // [P]
+};
+struct GaBestDev {
+    double* fit;
+    int* src;
+    int* updated;
+    float* ind;                 // [N*9]
+};
+hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
+                               const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
+                               float* off);
+hipError_t launch_ga_survivors(hipStream_t st, const float* fits, const float* off_fits, int P,
+                               int elite_k, int* src, float* new_fits, const GaBestDev& best,
+                               double* curves_row, int init);
+hipError_t launch_ga_gather(hipStream_t st, const float* pop, const float* off, int P, int N,
+                            const int* src, float* next, const GaBestDev& best, int init);
+int ga_max_population();
+
 }  // namespace ggs

@@ -17,6 +17,28 @@ GGS_FIT_NONE, GGS_FIT_WEIGHTED, GGS_FIT_BOOST = 0, 1, 2
 
 _f32p = C.POINTER(C.c_float)
 _i32p = C.POINTER(C.c_int32)
+_f64p = C.POINTER(C.c_double)
+
+
+class GaConfig(C.Structure):
+    """ggs_ga_config (include/ggs.h)."""
+    _fields_ = [("pop_size", C.c_int32), ("n_splats", C.c_int32), ("H", C.c_int32),
+                ("W", C.c_int32), ("tour_k", C.c_int32), ("elite_k", C.c_int32),
+                ("cxpb", C.c_float), ("mutpb", C.c_float), ("k_sigma", C.c_float),
+                ("min_scale_splats", C.c_float), ("max_scale_splats", C.c_float),
+                ("scale_log_lo", C.c_float), ("scale_log_hi", C.c_float),
+                ("fitness_mode", C.c_int32), ("boost_beta", C.c_float), ("schedule", C.c_int32),
+                ("sig_max", C.c_double * 6), ("sig_min", C.c_double * 6), ("seed", C.c_uint64)]
+
+
+class GaDraws(C.Structure):
+    """ggs_ga_draws (include/ggs.h)."""
+    _fields_ = [("tour_idx", _i32p), ("perm", _i32p), ("cx", _i32p), ("cx_u", _f32p),
+                ("u_xy", _f32p), ("u_ab", _f32p), ("u_t", _f32p), ("u_rgb", _f32p),
+                ("u_a", _f32p), ("k_color", _i32p), ("k_xy", _i32p), ("k_ab", _i32p),
+                ("k_t", _i32p), ("n_xy", _f32p), ("n_ab", _f32p), ("n_t", _f32p),
+                ("n_rgba", _f32p), ("swap_i", _i32p), ("swap_pick", _i32p), ("swap_u", _f64p)]
+
 
 # name -> (restype, argtypes); mirrors include/ggs.h one-for-one
 SIGNATURES = {
@@ -42,6 +64,12 @@ SIGNATURES = {
     "ggs_profile_enable": (C.c_int, [C.c_int32]),
     "ggs_profile_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "ggs_profile_reset": (None, []),
+    "ggs_ga_create": (C.c_int, [C.c_int32, C.POINTER(GaConfig), _f32p, _f32p, _f32p,
+                                C.POINTER(C.c_void_p)]),
+    "ggs_ga_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(GaDraws)]),
+    "ggs_ga_run": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    "ggs_ga_read": (C.c_int, [C.c_void_p, _f32p, _f32p, _f32p, _f64p, _f64p, _i32p]),
+    "ggs_ga_destroy": (None, [C.c_void_p]),
 }
 
 

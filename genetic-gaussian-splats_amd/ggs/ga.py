@@ -329,13 +329,17 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
                    *, seed: Optional[int] = None, draws=None,
                    evaluate: Optional[Callable[[np.ndarray], np.ndarray]] = None,
                    init_population: Optional[np.ndarray] = None, progress: bool = True,
-                   return_state: bool = False):
+                   return_state: bool = False, backend: str = "host", chunk: int = 50):
     """algorithm.py:17-195 → (best individual [N, 9] float32, best fitness).
 
     Extra keyword-only hooks: ``seed`` / ``draws`` (draw source), ``evaluate``
     (population [P,N,9] → fitness [P]; default: one libggs launch with the
     importance mask), ``init_population``, ``return_state`` (also return the
-    final population, fitnesses and curves)."""
+    final population, fitnesses and curves), ``backend``: "host" (numpy
+    operators, one libggs fitness launch per generation) or "device" (the whole
+    generation on the GPU, ggs/ga_device.py; Philox draws keyed by ``seed``, or
+    the draws a ``ga_device.RecordingDraws`` holds; ``chunk`` generations per
+    host call)."""
     from .mask import compute_importance_mask, prepare_target
 
     t = prepare_target(target_img_uint8, H, W)                         # algorithm.py:33-39
@@ -347,10 +351,19 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
 
         def evaluate(G):
             return api.fitness(G, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only)
-    draws = draws if draws is not None else NumpyDraws(seed)
     pop = (np.array(init_population, np.float32, copy=True) if init_population is not None else
            new_population(pop_size, n_splats, H, W, min_scale_splats, max_scale_splats,
                           np.random.default_rng(seed)))
+    if backend == "device":
+        return _genetic_approx_device(t, imp_mask, pop, H, W, generations, tour_k, elite_k, cxpb,
+                                      mutpb, mut_sigma_max, mut_sigma_min, schedule,
+                                      min_scale_splats, max_scale_splats, k_sigma, boost_only,
+                                      save_video, frame_every, video_dir, prefix, loss_png_path,
+                                      loss_csv_path, loss_log_y, seed, draws, progress,
+                                      return_state, chunk)
+    if backend != "host":
+        raise ValueError(f"backend must be 'host' or 'device', got {backend!r}")
+    draws = draws if draws is not None else NumpyDraws(seed)
     fits = np.asarray(evaluate(pop), np.float32)
 
     best_idx = int(np.argmin(fits))
@@ -408,4 +421,63 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
     save_curves_csv(curves, loss_csv_path)
     if return_state:
         return best_ind, best_fit, {"population": pop, "fitness": fits, "curves": curves}
+    return best_ind, best_fit
+
+
+def _genetic_approx_device(t, imp_mask, pop, H, W, generations, tour_k, elite_k, cxpb, mutpb,
+                           mut_sigma_max, mut_sigma_min, schedule, min_scale_splats,
+                           max_scale_splats, k_sigma, boost_only, save_video, frame_every,
+                           video_dir, prefix, loss_png_path, loss_csv_path, loss_log_y, seed,
+                           draws, progress, return_state, chunk):
+    """genetic_approx with backend="device" (ggs/ga_device.py)."""
+    from .ga_device import run_device_ga
+    pad = len(str(generations))
+    every = max(1, frame_every)
+    step = max(1, chunk)
+    if save_video:
+        step = math.gcd(step, every)                  # land on every frame generation
+    bar = None
+    if progress:
+        try:
+            from tqdm.auto import tqdm
+            bar = tqdm(total=generations, desc="GA generations (device)", leave=True)
+        except ImportError:
+            pass
+    state = {"gen": 0}
+
+    def on_chunk(gen, ga):
+        if bar is not None:
+            bar.update(gen - state["gen"])
+        state["gen"] = gen
+        if save_video and gen % every == 0:
+            st = ga.read()
+            save_frame_png(gen, st["best"], pad, prefix, video_dir, H, W, k_sigma, None, save_video)
+        if bar is not None:
+            bar.set_postfix(sigma_fac=f"{anneal_factor(gen, generations, schedule):.3f}")
+
+    if save_video:
+        from . import api
+        f0 = api.fitness(pop, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only)
+        save_frame_png(0, pop[int(np.argmin(f0))], pad, prefix, video_dir, H, W, k_sigma, None,
+                       save_video)
+    replay = getattr(draws, "generations", None) if draws is not None else None
+    try:
+        st = run_device_ga(t, imp_mask, pop, generations, tour_k=tour_k, elite_k=elite_k,
+                           cxpb=cxpb, mutpb=mutpb, mut_sigma_max=mut_sigma_max,
+                           mut_sigma_min=mut_sigma_min, schedule=schedule,
+                           min_scale_splats=min_scale_splats, max_scale_splats=max_scale_splats,
+                           k_sigma=k_sigma, boost_only=boost_only,
+                           seed=(int(np.random.SeedSequence().entropy) if seed is None else int(seed)) & (2**64 - 1), chunk=step, on_chunk=on_chunk,
+                           draws=replay)
+    finally:
+        if bar is not None:
+            bar.close()
+    curves = st["curves"]
+    save_loss_curve_png(curves, loss_png_path, title=f"{prefix} fitness", xlabel="Generation",
+                        ylabel="MSE", log_y=loss_log_y, dpi=144)
+    save_curves_csv(curves, loss_csv_path)
+    best_ind, best_fit = st["best"], st["best_fit"]
+    if return_state:
+        return best_ind, best_fit, {"population": st["population"], "fitness": st["fitness"],
+                                    "curves": curves}
     return best_ind, best_fit

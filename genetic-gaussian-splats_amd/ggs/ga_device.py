@@ -1,0 +1,179 @@
+"""Device-resident GA loop (ggs_ga_* in include/ggs.h, kernels in csrc/ggs_ga.hip).
+
+The whole generation of algorithm.py:85-155 — selection, crossover, mutation,
+fitness, elites, best individual, curves — runs on one GPU with no host round
+trip; the host only enqueues.  ``DeviceGA.step(draws=...)`` accepts explicit
+draws in ggs/ga.py's layout (tests/test_gpu_parity.py feeds it the same draws as
+the host path and requires identical populations); ``DeviceGA.run`` uses the
+in-kernel Philox stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import GaConfig, GaDraws, check, lib
+
+_f32p = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int32)
+_f64p = C.POINTER(C.c_double)
+SIG_KEYS = ("xy", "alog", "blog", "theta", "rgb", "alpha")
+SCHEDULES = {"linear": 0, "cosine": 1, "exp": 2}
+
+
+def _arr(x, dt):
+    return np.ascontiguousarray(x, dtype=dt)
+
+
+class DeviceGA:
+    """One device-resident GA population (see module docstring)."""
+
+    def __init__(self, target, mask, init_pop, *, tour_k: int, elite_k: int, cxpb: float,
+                 mutpb: float, mut_sigma_max: Dict[str, float], mut_sigma_min: Dict[str, float],
+                 schedule: str, min_scale_splats: float, max_scale_splats: float,
+                 k_sigma: float = 3.0, boost_only: bool = False, boost_beta: float = 1.0,
+                 seed: int = 0, device: int = 0):
+        from .ga import scale_log_bounds
+        pop = _arr(init_pop, np.float32)
+        P, N, Cc = pop.shape
+        if Cc != 9:
+            raise _lib.GGSInputError("the device GA keeps [P, N, 9] genomes")
+        self.target = _arr(target, np.float32)
+        H, W = self.target.shape[:2]
+        self.mask = None if mask is None else _arr(mask, np.float32)
+        lo, hi = scale_log_bounds(H, W, min_scale_splats, max_scale_splats)
+        cfg = GaConfig(P, N, H, W, tour_k, elite_k, cxpb, mutpb, k_sigma, min_scale_splats,
+                       max_scale_splats, float(lo), float(hi),
+                       _lib.GGS_FIT_NONE if self.mask is None else
+                       (_lib.GGS_FIT_BOOST if boost_only else _lib.GGS_FIT_WEIGHTED),
+                       boost_beta, SCHEDULES.get(schedule, 0),
+                       (C.c_double * 6)(*[mut_sigma_max[k] for k in SIG_KEYS]),
+                       (C.c_double * 6)(*[mut_sigma_min[k] for k in SIG_KEYS]), seed & (2**64 - 1))
+        self.P, self.N, self.H, self.W, self.tour_k, self.cxpb = P, N, H, W, tour_k, cxpb
+        _lib.ensure_init()
+        h = C.c_void_p()
+        check(lib.ggs_ga_create(device, C.byref(cfg), self.target.ctypes.data_as(_f32p),
+                                None if self.mask is None else self.mask.ctypes.data_as(_f32p),
+                                pop.ctypes.data_as(_f32p), C.byref(h)), "ggs_ga_create")
+        self.h = h
+
+    def step(self, gen: int, total: int, draws: Optional[Dict[str, np.ndarray]] = None) -> None:
+        """One generation; ``draws`` in ggs/ga.py layout (see draws_from_host)."""
+        if draws is None:
+            check(lib.ggs_ga_step(self.h, gen, total, None), "ggs_ga_step")
+            return
+        keep = {}
+        d = GaDraws()
+        for name, typ in GaDraws._fields_:
+            dt = np.float64 if name == "swap_u" else (np.int32 if typ is _i32p else np.float32)
+            a = keep[name] = _arr(draws[name], dt)
+            setattr(d, name, a.ctypes.data_as(typ))
+        check(lib.ggs_ga_step(self.h, gen, total, C.byref(d)), "ggs_ga_step")
+
+    def run(self, first_gen: int, n_gens: int, total: int) -> None:
+        check(lib.ggs_ga_run(self.h, first_gen, n_gens, total), "ggs_ga_run")
+
+    def read(self) -> Dict[str, object]:
+        pop = np.empty((self.P, self.N, 9), np.float32)
+        fits = np.empty(self.P, np.float32)
+        best = np.empty((self.N, 9), np.float32)
+        bf = C.c_double()
+        n = C.c_int32()
+        check(lib.ggs_ga_read(self.h, None, None, None, None, None, C.byref(n)), "ggs_ga_read")
+        curves = np.empty((n.value, 3), np.float64)
+        check(lib.ggs_ga_read(self.h, pop.ctypes.data_as(_f32p), fits.ctypes.data_as(_f32p),
+                              best.ctypes.data_as(_f32p), C.byref(bf),
+                              curves.ctypes.data_as(_f64p), C.byref(n)), "ggs_ga_read")
+        return {"population": pop, "fitness": fits, "best": best, "best_fit": bf.value,
+                "curves": {"best": curves[:, 0].tolist(), "mean": curves[:, 1].tolist(),
+                           "median": curves[:, 2].tolist()}}
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib.ggs_ga_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 — interpreter shutdown
+            pass
+
+
+def draws_from_host(tour_idx, perm, cx, cxu_compact, mut, N: int) -> Dict[str, np.ndarray]:
+    """Pack the draws ggs/ga.py's next_generation consumed into the device layout
+    (crossover masks expanded to one row per pair)."""
+    npairs = len(cx)
+    cx_u = np.ones((npairs, N), np.float32)
+    cx_u[np.asarray(cx, bool)] = np.asarray(cxu_compact, np.float32).reshape(-1, N)
+    out = {"tour_idx": tour_idx, "perm": perm, "cx": np.asarray(cx, np.int32), "cx_u": cx_u}
+    out.update({k: mut[k] for k in ("u_xy", "u_ab", "u_t", "u_rgb", "u_a", "k_color", "k_xy",
+                                    "k_ab", "k_t", "n_xy", "n_ab", "n_t", "n_rgba", "swap_i",
+                                    "swap_pick", "swap_u")})
+    return out
+
+
+class RecordingDraws:
+    """Wraps a ggs.ga draw source and keeps, per generation, the draws
+    ``next_generation`` consumed — in the device layout (``draws_from_host``)."""
+
+    def __init__(self, inner, cxpb: float):
+        self.inner, self.cxpb = inner, cxpb
+        self.generations = []
+        self._cur = {}
+
+    def tournament(self, P, k):
+        self._cur = {"tour_idx": np.asarray(self.inner.tournament(P, k))}
+        return self._cur["tour_idx"]
+
+    def shuffle(self, P):
+        self._cur["perm"] = np.asarray(self.inner.shuffle(P))
+        return self._cur["perm"]
+
+    def uniform(self, n):
+        u = np.asarray(self.inner.uniform(n))
+        self._cur["cx"] = u < self.cxpb
+        return u
+
+    def generation(self, cx, n_off, N, mutpb):
+        cxu, mut = self.inner.generation(cx, n_off, N, mutpb)
+        c = self._cur
+        self.generations.append(draws_from_host(c["tour_idx"], c["perm"], c["cx"], cxu, mut, N))
+        return cxu, mut
+
+
+def run_device_ga(target, imp_mask, init_pop, generations: int, *, tour_k: int, elite_k: int,
+                  cxpb: float, mutpb: float, mut_sigma_max, mut_sigma_min, schedule: str,
+                  min_scale_splats: float, max_scale_splats: float, k_sigma: float,
+                  boost_only: bool, seed: int, chunk: int, on_chunk=None, draws=None):
+    """algorithm.py:85-155 for ``generations`` generations on one GPU.
+
+    ``draws``: optional list of per-generation draw dicts (replay); otherwise the
+    Philox stream keyed by ``seed``.  ``on_chunk(gen, ga)`` runs every ``chunk``
+    generations (progress bar, video frames)."""
+    ga = DeviceGA(target, imp_mask, init_pop, tour_k=tour_k, elite_k=elite_k, cxpb=cxpb,
+                  mutpb=mutpb, mut_sigma_max=mut_sigma_max, mut_sigma_min=mut_sigma_min,
+                  schedule=schedule, min_scale_splats=min_scale_splats,
+                  max_scale_splats=max_scale_splats, k_sigma=k_sigma, boost_only=boost_only,
+                  seed=seed)
+    try:
+        gen = 1
+        try:
+            while gen <= generations:
+                n = min(max(1, chunk), generations - gen + 1)
+                if draws is not None:
+                    for g in range(gen, gen + n):
+                        ga.step(g, generations, draws[g - 1])
+                else:
+                    ga.run(gen, n, generations)
+                gen += n
+                if on_chunk is not None:
+                    on_chunk(gen - 1, ga)
+        except KeyboardInterrupt:                                  # algorithm.py:157-158
+            print("\n[Interrupted] Returning current best individual…", flush=True)
+        return ga.read()
+    finally:
+        ga.close()

@@ -115,6 +115,49 @@ int ggs_fitness_device(int32_t device, void* stream, const float* d_genomes_axes
                        int32_t mode, float boost_beta, int32_t H, int32_t W, float k_sigma,
                        float* d_out_B);
 
+/* ---- device-resident GA ------------------------------
+ * genetic_approx's generation loop (algorithm.py:85-155) on one device: the
+ * population, fitness, elites, best individual and curves stay in HBM; a
+ * generation is variation -> fitness -> survivors -> gather, no host sync.
+ * Draws: explicit arrays (ggs_ga_step with draws != NULL; replay / parity) or a
+ * counter-based Philox4x32-10 stream keyed by (seed, generation, individual). */
+typedef struct ggs_ga_config {
+    int32_t pop_size, n_splats, H, W, tour_k, elite_k;
+    float cxpb, mutpb, k_sigma, min_scale_splats, max_scale_splats;
+    float scale_log_lo, scale_log_hi; /* clamp bounds log(min), log(max*max(H,W)); 0,0 = compute */
+    int32_t fitness_mode;             /* GGS_FIT_* */
+    float boost_beta;
+    int32_t schedule;                 /* 0 linear, 1 cosine, 2 exp (utils.py:14-27) */
+    double sig_max[6], sig_min[6];    /* xy, alog, blog, theta, rgb, alpha (config.py:22-43) */
+    uint64_t seed;
+} ggs_ga_config;
+
+typedef struct ggs_ga_draws {         /* host arrays for ONE generation (ggs/ga.py layout) */
+    const int32_t* tour_idx;          /* [P*k]   random.randrange draws (genetic.py:11) */
+    const int32_t* perm;              /* [P]     random.shuffle (algorithm.py:90) */
+    const int32_t* cx;                /* [ceil(P/2)] crossover decisions (algorithm.py:97) */
+    const float* cx_u;                /* [ceil(P/2)*N] crossover masks (genetic.py:18) */
+    const float *u_xy, *u_ab;         /* [P*N*2] mask uniforms (genetic.py:37-38) */
+    const float *u_t, *u_rgb, *u_a;   /* [P*N] */
+    const int32_t *k_color, *k_xy, *k_ab, *k_t;   /* [P] one-true fallbacks (genetic.py:24-29) */
+    const float *n_xy, *n_ab;         /* [P*N*2] normals (genetic.py:57-70) */
+    const float* n_t;                 /* [P*N] */
+    const float* n_rgba;              /* [P*N*4] */
+    const int32_t *swap_i, *swap_pick;/* [P] swap draws (genetic.py:79-91); pick < 0 -> swap_u */
+    const double* swap_u;             /* [P] */
+} ggs_ga_draws;
+
+/* init_pop [P,N,9] axes-angle (required); mask may be NULL iff fitness_mode is
+ * GGS_FIT_NONE.  Evaluates the initial population. */
+int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_hw3,
+                  const float* mask_hw, const float* init_pop, void** handle);
+int ggs_ga_step(void* handle, int32_t gen, int32_t total_gens, const ggs_ga_draws* draws);
+int ggs_ga_run(void* handle, int32_t first_gen, int32_t n_gens, int32_t total_gens);
+/* Synchronises; any output may be NULL.  curves: [n_curves][3] = best, mean, median. */
+int ggs_ga_read(void* handle, float* pop, float* fits, float* best_ind, double* best_fit,
+                double* curves, int32_t* n_curves);
+void ggs_ga_destroy(void* handle);
+
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------
  * When enabled, every launch of "prep", "raster" and "finalize" is bracketed
  * by hipEvents; ggs_profile_read synchronises those events and returns the

@@ -1,0 +1,146 @@
+"""The device-resident GA (ggs/ga_device.py, csrc/ggs_ga.hip) on an MI355X.
+
+Bars:
+* fed the SAME draws as the host GA (ggs/ga.py, itself replay-verified against
+  the reference in tests/test_ga.py), every generation's population, fitness
+  vector, best individual and curves are IDENTICAL (bit-exact);
+* fed the reference's own recorded draws (tests/golden/ga_loop.npz), the
+  offspring and elites are the reference's genomes bit for bit and the fitness
+  values within the evaluator bar (rel 1e-5);
+* with the in-kernel Philox draws: operators keep genomes in range, curves are
+  monotone, the best fitness is what the evaluator returns for the best genome,
+  runs are reproducible per seed.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import ggs
+from conftest import load_golden
+from ggs import ga
+from ggs.ga_device import DeviceGA, RecordingDraws
+from ggs.mask import compute_importance_mask, prepare_target
+
+pytestmark = pytest.mark.gpu
+CFG = dict(mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0,
+                          "alpha": 25.0},
+           mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0,
+                          "alpha": 2.0},
+           schedule="cosine")          # reference modules/config.py:22-43
+MIN_S, MAX_S = 3.0, 0.1
+
+
+def _problem(H, W, seed):
+    target = np.random.default_rng(seed).uniform(0, 255, (H + 9, W + 5, 3)).astype(np.float32)
+    t = prepare_target(target, H, W)
+    return target, t, compute_importance_mask(t, H, W, smooth=3, strength=0.7)
+
+
+@pytest.mark.parametrize("H,W,P,N,G,tour_k,elite_k,cxpb,mutpb,boost,seed", [
+    (40, 40, 17, 33, 4, 3, 4, 0.5, 0.2, False, 1),     # odd P (last pair yields one child)
+    (64, 48, 32, 300, 3, 2, 8, 0.9, 0.05, True, 2),    # N > 256: multi-pass workgroup loops
+    (32, 32, 8, 2, 5, 2, 1, 0.3, 0.01, False, 3),      # N = 2, rare mutation -> fallbacks
+    (24, 24, 6, 1, 3, 2, 0, 0.5, 0.5, False, 4),       # N = 1: no swap; elite_k 0 -> 1
+])
+def test_device_ga_matches_host_ga_with_same_draws(H, W, P, N, G, tour_k, elite_k, cxpb, mutpb,
+                                                    boost, seed):
+    target, t, m = _problem(H, W, seed)
+    init = ga.new_population(P, N, H, W, MIN_S, MAX_S, np.random.default_rng(seed))
+    rec = RecordingDraws(ga.NumpyDraws(seed), cxpb)
+    kw = dict(pop_size=P, n_splats=N, generations=G, tour_k=tour_k, elite_k=elite_k, cxpb=cxpb,
+              mutpb=mutpb, min_scale_splats=MIN_S, max_scale_splats=MAX_S, k_sigma=3.0,
+              mask_strength=0.7, boost_only=boost, init_population=init, progress=False,
+              return_state=True, **CFG)
+    hb, hf, hs = ga.genetic_approx(target, H, W, "cuda", draws=rec, **kw)
+    assert len(rec.generations) == G
+    db, df, ds = ga.genetic_approx(target, H, W, "cuda", draws=rec, backend="device", chunk=2, **kw)
+    np.testing.assert_array_equal(ds["population"], hs["population"])
+    np.testing.assert_array_equal(ds["fitness"], hs["fitness"])
+    np.testing.assert_array_equal(db, hb)
+    assert df == hf
+    for key in ("best", "mean", "median"):
+        assert ds["curves"][key] == hs["curves"][key], key
+
+
+def test_device_ga_replays_reference_draws():
+    """Draws recorded from the reference's genetic_approx → the reference's genomes."""
+    from test_ga import ReplayDraws
+    d = load_golden("ga_loop.npz")
+    H, W, P, N, G, tour_k, elite_k, cxpb, mutpb = d["cfg"]
+    H, W, P, N, G, tour_k, elite_k = (int(v) for v in (H, W, P, N, G, tour_k, elite_k))
+    # collect the per-generation draws by running the host GA on the reference's fitness
+    calls = []
+
+    def evaluate(pop):
+        k = len(calls)
+        ref_call = 0 if k == 0 else 2 * k - 1
+        calls.append(ref_call)
+        return d[f"call{ref_call}__fit"].astype(np.float32)
+
+    rec = RecordingDraws(ReplayDraws(d), float(cxpb))
+    ga.genetic_approx(d["target"], H, W, "cuda", pop_size=P, n_splats=N, generations=G,
+                      tour_k=tour_k, elite_k=elite_k, cxpb=float(cxpb), mutpb=float(mutpb),
+                      min_scale_splats=MIN_S, max_scale_splats=MAX_S, k_sigma=3.0,
+                      mask_strength=0.7, boost_only=False, draws=rec, evaluate=evaluate,
+                      init_population=d["init"], progress=False, **CFG)
+    t = prepare_target(d["target"], H, W)
+    m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
+    dga = DeviceGA(t, m, d["init"], tour_k=tour_k, elite_k=elite_k, cxpb=float(cxpb),
+                   mutpb=float(mutpb), min_scale_splats=MIN_S, max_scale_splats=MAX_S, **CFG)
+    try:
+        E = max(1, elite_k)
+        for g in range(1, G + 1):
+            dga.step(g, G, rec.generations[g - 1])
+            st = dga.read()
+            off = d[f"call{2 * g - 1}__pop"]                 # the reference's offspring
+            np.testing.assert_array_equal(st["population"][E:], off[:P - E], err_msg=f"gen {g}")
+            np.testing.assert_allclose(st["fitness"][E:], d[f"call{2 * g - 1}__fit"][:P - E],
+                                       rtol=1e-5)
+            np.testing.assert_array_equal(st["population"][:E], d[f"call{2 * g}__pop"])
+        np.testing.assert_array_equal(st["best"], d["best"])
+        assert st["best_fit"] == pytest.approx(float(d["best_fit"]), rel=1e-5)
+        np.testing.assert_allclose(st["curves"]["best"], d["curve__best"], rtol=1e-5)
+        np.testing.assert_allclose(st["curves"]["mean"], d["curve__mean"], rtol=1e-5)
+        np.testing.assert_allclose(st["curves"]["median"], d["curve__median"], rtol=1e-5)
+    finally:
+        dga.close()
+
+
+def test_device_ga_philox_run():
+    H = W = 64
+    P, N, G = 48, 64, 30
+    target, t, m = _problem(H, W, 7)
+    kw = dict(pop_size=P, n_splats=N, generations=G, tour_k=3, elite_k=4, cxpb=0.3, mutpb=0.1,
+              min_scale_splats=MIN_S, max_scale_splats=MAX_S, k_sigma=3.0, mask_strength=0.7,
+              boost_only=False, progress=False, return_state=True, backend="device", **CFG)
+    b1, f1, s1 = ga.genetic_approx(target, H, W, "cuda", seed=11, chunk=7, **kw)
+    c = s1["curves"]["best"]
+    assert len(c) == G + 1 and all(y <= x for x, y in zip(c, c[1:])) and c[-1] < c[0]
+    assert float(ggs.fitness(b1[None], t, H, W, 3.0, weight_mask=m)[0]) == f1 == c[-1]
+    np.testing.assert_array_equal(ggs.fitness(s1["population"], t, H, W, 3.0, weight_mask=m),
+                                  s1["fitness"])
+    Pp = s1["population"]
+    assert (Pp[..., 0:2] >= 0).all() and (Pp[..., 0:2] <= 1).all()
+    lo, hi = ga.scale_log_bounds(H, W, MIN_S, MAX_S)
+    assert (Pp[..., 2:4] >= lo).all() and (Pp[..., 2:4] <= hi).all()
+    assert (Pp[..., 4] >= -np.pi - 1e-6).all() and (Pp[..., 4] < np.pi + 1e-6).all()
+    assert (Pp[..., 5:9] >= 0).all() and (Pp[..., 5:9] <= 255).all()
+    # reproducible per seed and chunking-independent; another seed differs
+    b2, f2, s2 = ga.genetic_approx(target, H, W, "cuda", seed=11, chunk=30, **kw)
+    np.testing.assert_array_equal(s2["population"], s1["population"])
+    assert f2 == f1
+    _, _, s3 = ga.genetic_approx(target, H, W, "cuda", seed=12, chunk=30, **kw)
+    assert not np.array_equal(s3["population"], s1["population"])
+
+
+def test_device_ga_rejects_bad_config():
+    H = W = 16
+    _, t, m = _problem(H, W, 0)
+    init = ga.new_population(4, 3, H, W, MIN_S, MAX_S, np.random.default_rng(0))
+    with pytest.raises(AssertionError):
+        DeviceGA(t, m, init, tour_k=0, elite_k=1, cxpb=0.5, mutpb=0.1, min_scale_splats=MIN_S,
+                 max_scale_splats=MAX_S, **CFG)
+    with pytest.raises(AssertionError):
+        DeviceGA(t, m, init, tour_k=2, elite_k=5, cxpb=0.5, mutpb=0.1, min_scale_splats=MIN_S,
+                 max_scale_splats=MAX_S, **CFG)

@@ -2,7 +2,11 @@
 workload (512x512, 256 splats, pop 128) — host-side batched operators + one
 libggs launch per generation — with the host/device split.
 
-usage: python tools/bench_ga.py [--gens 200] [--pop 128] [--splats 256] [--size 512]"""
+--backend device: the device-resident loop (ggs/ga_device.py), whole generations
+on the GPU (Philox draws), timed around DeviceGA.run + a final read.
+
+usage: python tools/bench_ga.py [--gens 200] [--pop 128] [--splats 256] [--size 512]
+                                [--backend host|device]"""
 import argparse, json, os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -15,6 +19,7 @@ ap.add_argument("--gens", type=int, default=200)
 ap.add_argument("--pop", type=int, default=128)
 ap.add_argument("--splats", type=int, default=256)
 ap.add_argument("--size", type=int, default=512)
+ap.add_argument("--backend", default="host", choices=["host", "device"])
 a = ap.parse_args()
 H = W = a.size
 target = np.random.default_rng(0).uniform(0, 255, (H, W, 3)).astype(np.float32)
@@ -25,6 +30,26 @@ t_eval = [0.0]
 from ggs.mask import compute_importance_mask, prepare_target
 t = prepare_target(target, H, W)
 m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
+
+if a.backend == "device":
+    from ggs.ga_device import DeviceGA
+    init = ga.new_population(a.pop, a.splats, H, W, 3.0, 0.1, np.random.default_rng(0))
+    dga = DeviceGA(t, m, init, tour_k=2, elite_k=8, cxpb=0.05, mutpb=0.05, min_scale_splats=3.0,
+                   max_scale_splats=0.1, seed=1, **cfg)
+    dga.run(1, 5, a.gens)                                          # warm-up
+    dga.read()
+    t0 = time.perf_counter()
+    dga.run(6, a.gens, a.gens + 5)
+    st = dga.read()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"metric": "GA generations/s (device-resident)", "value": round(a.gens / dt, 2),
+                      "config": {"H": H, "W": W, "splats": a.splats, "pop": a.pop, "gens": a.gens},
+                      "ms_per_gen": round(dt / a.gens * 1e3, 4),
+                      "candidate_renders_per_s": round(a.gens * a.pop / dt, 1),
+                      "best_fit": st["best_fit"]}))
+    dga.close()
+    sys.exit(0)
+
 
 def evaluate(G):
     t0 = time.perf_counter()
