@@ -1,0 +1,168 @@
+"""Simulated annealing around the MI355X evaluator (SURVEY.md §8f next #4;
+BASELINE configs[4]: run_sags.py, 2048², 4096 splats, 8 tries per iteration).
+
+Restates annealing.py:19-190 with one change of *schedule*, not of result:
+the reference evaluates its ``tries_per_iter`` neighbours one launch at a time
+because each try mutates the CURRENT state, which an acceptance changes.  The
+mutation draws do not depend on the state (``NumpyDraws`` draws fixed-size
+arrays; the reference's torch stream is separate from the Python stream the
+acceptance test uses), so here the remaining tries of an iteration are
+mutated from the current state and evaluated in ONE batched libggs launch;
+the acceptance test then walks them in order, and on the first acceptance the
+rest of the batch is discarded and re-mutated from the new state with the
+same draws.  The accepted sequence, the acceptance draws consumed, the best
+individual and the curves are exactly the sequential loop's
+(tests/test_sa.py replays the reference's recorded draws through both widths).
+
+``speculate`` bounds the batch width: None adapts it to the observed
+acceptance rate (wide when moves are rarely accepted — the common case at low
+temperature — narrow when most are).
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Optional
+
+import numpy as np
+
+from .ga import (NumpyDraws, mutate_batch, new_population, save_curves_csv, save_frame_png,
+                 save_loss_curve_png)
+
+
+def temp_schedule(kind: str, T0: float, i: int, total: int) -> float:
+    """annealing.py:29-44."""
+    p = i / max(1, total)
+    if kind == "linear":
+        return max(1e-12, T0 * (1.0 - p))
+    if kind == "cosine":
+        return max(1e-12, T0 * 0.5 * (1.0 + math.cos(math.pi * p)))
+    if kind == "log":
+        return max(1e-12, T0 / (1.0 + math.log(1.0 + 9.0 * i)))
+    if kind == "cauchy":
+        return max(1e-12, T0 / (1.0 + i))
+    r = 0.01 ** (1.0 / max(1, total))                       # "exp" and the fallback
+    return T0 * (r ** i)
+
+
+def _slice(d, a: int, b: int):
+    return {k: np.asarray(v)[a:b] for k, v in d.items()}
+
+
+def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int, mutpb: float,
+                        mut_sigma_max: dict, mut_sigma_min: dict, sigma_schedule: str,
+                        min_scale_splats: float, max_scale_splats: float, k_sigma: float,
+                        mask_strength: float, boost_only: bool, iterations: int, temp0: float,
+                        temp_schedule: str, tries_per_iter: int = 1, save_video: bool = False,
+                        frame_every: int = 10_000, video_dir: str = "", prefix: str = "sa",
+                        loss_png_path: str = "", loss_csv_path: str = "",
+                        loss_log_y: bool = False, *, seed: Optional[int] = None, draws=None,
+                        evaluate: Optional[Callable[[np.ndarray], np.ndarray]] = None,
+                        init_individual: Optional[np.ndarray] = None, progress: bool = True,
+                        return_state: bool = False, speculate: Optional[int] = None):
+    """annealing.py:47-190 → (best individual [N, 9] float32, best energy).
+
+    Keyword-only hooks as ggs.ga.genetic_approx (``seed``, ``draws`` — a source
+    with ``mutation(n, N, mutpb)`` and ``accept()`` —, ``evaluate``,
+    ``init_individual``, ``return_state``) plus ``speculate`` (see module doc)."""
+    from .mask import compute_importance_mask, prepare_target
+    sched = temp_schedule
+    t = prepare_target(target_img_uint8, H, W)                       # annealing.py:87
+    imp_mask = compute_importance_mask(t, H, W, edge_scales=(1, 2, 4), w_edge=0.7, w_var=0.3,
+                                       gamma=0.7, floor=0.15, smooth=3,
+                                       strength=mask_strength)        # annealing.py:89-94
+    if evaluate is None:
+        from . import api
+
+        def evaluate(G):
+            return api.fitness(G, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only)
+    draws = draws if draws is not None else NumpyDraws(seed)
+    curr = (np.array(init_individual, np.float32, copy=True) if init_individual is not None else
+            new_population(1, n_splats, H, W, min_scale_splats, max_scale_splats,
+                           np.random.default_rng(seed))[0])
+    N = curr.shape[0]
+    curr_fit = float(np.asarray(evaluate(curr[None]), np.float32)[0])   # annealing.py:99-101
+    best = curr.copy()
+    best_fit = curr_fit
+    curves = {"best": [best_fit], "current": [curr_fit]}
+    pad = len(str(iterations))
+    if save_video:
+        save_frame_png(0, best, pad, prefix, video_dir, H, W, k_sigma, device, save_video)
+
+    tries = max(0, int(tries_per_iter))
+    acc_rate = 0.0                     # EWMA of the per-try acceptance rate
+    stats = {"evaluated": 0, "tries": 0, "launches": 0}
+    bar = range(iterations)
+    if progress:
+        try:
+            from tqdm.auto import tqdm
+            bar = tqdm(bar, desc="SA iterations", leave=True)
+        except ImportError:
+            pass
+    try:
+        for it in bar:
+            T = sched_T = _T(sched, temp0, it, iterations)
+            accepted_any = False
+            e_curr = float(curr_fit)
+            d = draws.mutation(tries, N, mutpb) if tries else None
+            k = 0
+            while k < tries:
+                if speculate is not None:
+                    w = max(1, int(speculate))
+                else:
+                    w = tries if acc_rate < 1.0 / tries else max(1, int(round(1.0 / acc_rate)))
+                w = min(w, tries - k)
+                nb = mutate_batch(np.repeat(curr[None], w, axis=0), _slice(d, k, k + w), it,
+                                  iterations, sigma_schedule, mut_sigma_max, mut_sigma_min, mutpb,
+                                  H, W, min_scale_splats, max_scale_splats)
+                e = np.asarray(evaluate(nb), np.float32)
+                stats["evaluated"] += w
+                stats["launches"] += 1
+                for j in range(w):
+                    e_new = float(e[j])
+                    dE = e_new - e_curr                                    # annealing.py:133
+                    acc = dE <= 0.0
+                    if not acc and T > 0.0:
+                        acc = draws.accept() < math.exp(-dE / T)           # annealing.py:140-142
+                    k += 1
+                    acc_rate = 0.9 * acc_rate + 0.1 * float(acc)
+                    if acc:
+                        curr = nb[j].copy()
+                        curr_fit = e_new
+                        e_curr = curr_fit
+                        accepted_any = True
+                    if e_curr + 1e-12 < best_fit:                          # annealing.py:148-150
+                        best_fit = e_curr
+                        best = curr.copy()
+                    if acc:
+                        break                  # the rest of the batch came from the old state
+            stats["tries"] += tries
+            curves["best"].append(best_fit)
+            curves["current"].append(float(curr_fit))
+            if save_video and (it + 1) % max(1, frame_every) == 0:
+                save_frame_png(it + 1, best, pad, prefix, video_dir, H, W, k_sigma, device, save_video)
+            if hasattr(bar, "set_postfix"):
+                bar.set_postfix(best_mse=f"{best_fit:.6f}", curr_mse=f"{float(curr_fit):.6f}",
+                                T=f"{sched_T:.4g}", accepted="Y" if accepted_any else "N")
+    except KeyboardInterrupt:
+        print("\n[Interrupted] Returning current best…", flush=True)
+    finally:
+        if hasattr(bar, "close"):
+            bar.close()
+
+    try:                                                                   # annealing.py:174-188
+        save_loss_curve_png(curves, loss_png_path, title=f"{prefix} energy (MSE)",
+                            xlabel="Iteration", ylabel="MSE", log_y=loss_log_y, dpi=144)
+        save_curves_csv(curves, loss_csv_path)
+        if loss_png_path:
+            print(f"Saved loss plot to {loss_png_path}")
+        if loss_csv_path:
+            print(f"Saved loss CSV to {loss_csv_path}")
+    except Exception as e:  # noqa: BLE001 — as the reference
+        print(f"[warn] Could not save SA curves: {e}")
+    if return_state:
+        return best, float(best_fit), {"current": curr, "current_fit": curr_fit,
+                                       "curves": curves, "stats": stats}
+    return best, float(best_fit)
+
+
+_T = temp_schedule

@@ -124,6 +124,9 @@ class NumpyDraws:
             "swap_u": r.random(P),
         }
 
+    def accept(self) -> float:                                     # random.random (annealing.py:142)
+        return float(self.rng.random())
+
     def generation(self, cx: np.ndarray, n_off: int, N: int, mutpb: float):
         """Crossover masks for the crossing pairs + mutation draws for the offspring."""
         return self.crossover_masks(int(cx.sum()), N), self.mutation(n_off, N, mutpb)
@@ -329,17 +332,18 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
                    *, seed: Optional[int] = None, draws=None,
                    evaluate: Optional[Callable[[np.ndarray], np.ndarray]] = None,
                    init_population: Optional[np.ndarray] = None, progress: bool = True,
-                   return_state: bool = False, backend: str = "host", chunk: int = 50):
+                   return_state: bool = False, backend: str = "auto", chunk: int = 50):
     """algorithm.py:17-195 → (best individual [N, 9] float32, best fitness).
 
     Extra keyword-only hooks: ``seed`` / ``draws`` (draw source), ``evaluate``
     (population [P,N,9] → fitness [P]; default: one libggs launch with the
     importance mask), ``init_population``, ``return_state`` (also return the
     final population, fitnesses and curves), ``backend``: "host" (numpy
-    operators, one libggs fitness launch per generation) or "device" (the whole
+    operators, one libggs fitness launch per generation), "device" (the whole
     generation on the GPU, ggs/ga_device.py; Philox draws keyed by ``seed``, or
     the draws a ``ga_device.RecordingDraws`` holds; ``chunk`` generations per
-    host call)."""
+    host call) or "auto" (device unless an ``evaluate`` or ``draws`` hook is
+    given)."""
     from .mask import compute_importance_mask, prepare_target
 
     t = prepare_target(target_img_uint8, H, W)                         # algorithm.py:33-39
@@ -354,6 +358,8 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
     pop = (np.array(init_population, np.float32, copy=True) if init_population is not None else
            new_population(pop_size, n_splats, H, W, min_scale_splats, max_scale_splats,
                           np.random.default_rng(seed)))
+    if backend == "auto":
+        backend = "device" if evaluate is None and draws is None else "host"
     if backend == "device":
         return _genetic_approx_device(t, imp_mask, pop, H, W, generations, tour_k, elite_k, cxpb,
                                       mutpb, mut_sigma_max, mut_sigma_min, schedule,

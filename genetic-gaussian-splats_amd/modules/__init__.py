@@ -1,8 +1,13 @@
-"""Drop-in replacements for the reference's hot-path modules.
+"""Drop-in replacements for the reference's ``modules`` package.
 
 Put ``genetic-gaussian-splats_amd/`` ahead of the reference checkout on
-``sys.path`` (or copy ``modules/render.py``, ``modules/fitness.py`` and
-``modules/encode.py`` over the reference's) and ``from modules.render import
-render_splats_rgb_triton`` / ``from modules.fitness import fitness_population``
-resolve to the MI355X implementation.  See INTEGRATION.md.
+``sys.path`` and ``from modules.render import render_splats_rgb_triton``,
+``modules.fitness``, ``modules.algorithm``, ``modules.annealing`` … resolve to
+the MI355X implementation.  Every other ``modules`` directory on ``sys.path``
+(the reference's) is appended to this package's search path, so modules not
+restated here — ``modules.config`` — still come from the reference checkout.
+See INTEGRATION.md.
 """
+from pkgutil import extend_path
+
+__path__ = extend_path(__path__, __name__)

@@ -139,19 +139,24 @@ def preprocess(genome, H: int, W: int, k_sigma: float = 3.0,
 
 
 def render(genomes, H: int, W: int, *, k_sigma: float = 3.0,
-           background=(1.0, 1.0, 1.0)) -> np.ndarray:
+           background=(1.0, 1.0, 1.0), window=None) -> np.ndarray:
     """render.py:203-252 semantics → float32 [B,H,W,3] clamped to [0,1].
 
     Per pixel (X, Y) (integer coordinates), for every splat whose integer AABB
     contains it, in ascending splat index (render.py:106-108 key order):
     quad = sxx·qx² + 2·sxy·qx·qy + syy·qy², f = exp(-0.5·quad)·a,
     C = (1-f)·C + f·c  (render.py:189-196).
+
+    ``window=(wy0, wy1, wx0, wx1)`` renders only rows wy0..wy1-1 and columns
+    wx0..wx1-1 of the H×W image (same values as the full render there), so
+    large configurations can be checked on a crop in seconds.
     """
     G = _as3d(genomes)
     B, N, C = G.shape
     if C < 9:
         raise ValueError("expected at least 9 genome cols")
-    img = np.empty((B, H, W, 3), np.float32)
+    wy0, wy1, wx0, wx1 = window if window is not None else (0, H, 0, W)
+    img = np.empty((B, wy1 - wy0, wx1 - wx0, 3), np.float32)
     img[:] = np.asarray(background, dtype=np.float32)
     two, mhalf, one = _f32(2.0), _f32(-0.5), _f32(1.0)
     for b in range(B):
@@ -159,6 +164,7 @@ def render(genomes, H: int, W: int, *, k_sigma: float = 3.0,
         canvas = img[b]
         for i in range(N):
             x0, x1, y0, y1 = (int(p[k_][i]) for k_ in BOUND_KEYS)
+            x0, x1, y0, y1 = max(x0, wx0), min(x1, wx1 - 1), max(y0, wy0), min(y1, wy1 - 1)
             if x1 < x0 or y1 < y0:
                 continue
             X = np.arange(x0, x1 + 1, dtype=np.float32)[None, :]
@@ -169,7 +175,7 @@ def render(genomes, H: int, W: int, *, k_sigma: float = 3.0,
                 + p["syy"][i] * (qy * qy)
             f = (np.exp(mhalf * quad) * p["a"][i])[..., None]
             col = np.array([p["rc"][i], p["gc"][i], p["bc"][i]], np.float32)
-            win = canvas[y0:y1 + 1, x0:x1 + 1]
+            win = canvas[y0 - wy0:y1 + 1 - wy0, x0 - wx0:x1 + 1 - wx0]
             win[...] = (one - f) * win + f * col
     np.clip(img, _f32(0.0), _f32(1.0), out=img)             # render.py:252
     return img

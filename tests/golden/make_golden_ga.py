@@ -13,6 +13,8 @@ batched operators and requires identical results.
                  (Triton interpreter renders): initial population, the Python
                  and torch draw streams, every fitness call's population and
                  values, final best and curves
+  sa_loop.npz    simulated_annealing (annealing.py:47-190), same recording, for
+                 three temperature schedules
 """
 from __future__ import annotations
 
@@ -34,6 +36,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import modules.algorithm as A  # noqa: E402  (reference)
+import modules.annealing as SA  # noqa: E402  (reference)
 import modules.config as CFG  # noqa: E402  (reference)
 import modules.fitness as F  # noqa: E402  (reference)
 import modules.genetic as GEN  # noqa: E402  (reference)
@@ -152,6 +155,99 @@ def mutate_fixture():
     np.savez_compressed(os.path.join(HERE, "ga_mutate.npz"), **out)
 
 
+def _streams(out, rtap, ttap, pre=""):
+    """Python stream: kinds 0 random, 1 randrange, 2 shuffle (perm stored
+    separately); torch stream: kinds 0 rand, 1 randn, 2 randint, flattened."""
+    py_kind, py_val, perms = [], [], []
+    for kind, v in rtap.log:
+        if kind == "shuffle":
+            py_kind.append(2)
+            py_val.append(len(perms))
+            perms.append(v)
+        else:
+            py_kind.append(0 if kind == "random" else 1)
+            py_val.append(v)
+    out[pre + "py_kind"] = np.array(py_kind, np.int64)
+    out[pre + "py_val"] = np.array(py_val, np.float64)
+    out[pre + "py_perms"] = np.array(perms, np.int64) if perms else np.zeros((0, 0), np.int64)
+    t_kind, t_shape, t_off, flat = [], [], [], []
+    off = 0
+    for kind, t in ttap.log:
+        t_kind.append({"rand": 0, "randn": 1, "randint": 2}[kind])
+        a = t.numpy().astype(np.float64).ravel()
+        t_shape.append(list(t.shape) + [0] * (2 - t.dim()) if t.dim() <= 2 else list(t.shape))
+        t_off.append(off)
+        flat.append(a)
+        off += a.size
+    out[pre + "t_kind"] = np.array(t_kind, np.int64)
+    out[pre + "t_shape"] = np.array(t_shape, np.int64)
+    out[pre + "t_off"] = np.array(t_off + [off], np.int64)
+    out[pre + "t_flat"] = np.concatenate(flat) if flat else np.zeros(0)
+
+
+def sa_fixture():
+    """simulated_annealing on CPU with recorded draws; cases differ in schedule,
+    T0 (random acceptance exercised) and tries per iteration."""
+    H, W, N = 32, 28, 10
+    target = np.random.default_rng(9).uniform(0, 255, (36, 30, 3)).astype(np.float32)
+    cases = [("cos", "cosine", 2e-3, 3, 6, 0.2), ("exp", "exp", 5e-2, 2, 5, 0.3),
+             ("log", "log", 0.0, 4, 3, 0.1), ("lin", "linear", 1e-2, 1, 6, 0.5),
+             ("cau", "cauchy", 1e-2, 2, 3, 0.2)]
+    out = {"target": target, "dims": np.array([H, W, N], np.int64)}
+    for name, sched, T0, tries, iters, mutpb in cases:
+        torch.manual_seed(7)
+        rtap = RandomTap(11)
+        ttap = TorchTap()
+        SA.random = rtap
+        GEN.random = rtap
+        GEN.torch = ttap
+        F.render_splats_rgb_triton = ref_render_cpu
+        rec = {"init": None, "calls": [], "curves": None}
+
+        def new_individual(*a, **k):
+            ind = torch.from_numpy(synthetic_population(1, N, H, W, seed=13)[0])
+            rec["init"] = ind.numpy().copy()
+            return ind
+
+        def fitness_population(population, *a, **k):
+            vals = F.fitness_population(population, *a, **k)
+            rec["calls"].append((np.stack([p.numpy() for p in population]), np.asarray(vals)))
+            return vals
+
+        def save_curves_csv(curves, path):
+            rec["curves"] = {k: np.asarray(v, np.float64) for k, v in curves.items()}
+
+        SA.new_individual = new_individual
+        SA.fitness_population = fitness_population
+        SA.prewarm_renderer = lambda *a, **k: None
+        SA.save_curves_csv = save_curves_csv
+        SA.save_loss_curve_png = lambda *a, **k: None
+        best, best_fit = SA.simulated_annealing(
+            torch.from_numpy(target), H=H, W=W, device="cpu", n_splats=N, mutpb=mutpb,
+            mut_sigma_max=CFG.MUT_SIGMA_MAX, mut_sigma_min=CFG.MUT_SIGMA_MIN,
+            sigma_schedule=CFG.SCHEDULE, min_scale_splats=CFG.MIN_SCALE_SPLATS,
+            max_scale_splats=CFG.MAX_SCALE_SPLATS, k_sigma=3.0, mask_strength=0.7,
+            boost_only=name == "exp", iterations=iters, temp0=T0, temp_schedule=sched,
+            tries_per_iter=tries, loss_csv_path="unused.csv")
+        pre = name + "__"
+        out[pre + "cfg"] = np.array([iters, tries, T0, mutpb, name == "exp"], np.float64)
+        out[pre + "sched"] = np.array(sched)
+        out[pre + "init"] = rec["init"]
+        out[pre + "best"] = best.numpy()
+        out[pre + "best_fit"] = np.float64(best_fit)
+        out[pre + "n_calls"] = np.int64(len(rec["calls"]))
+        for i, (pop, vals) in enumerate(rec["calls"]):
+            out[pre + f"call{i}__pop"] = pop
+            out[pre + f"call{i}__fit"] = vals
+        for k, v in rec["curves"].items():
+            out[pre + f"curve__{k}"] = v
+        _streams(out, rtap, ttap, pre)
+        print("sa", name, "best_fit", best_fit, "calls", len(rec["calls"]),
+              "accept draws", sum(1 for k, _ in rtap.log if k == "random"))
+    GEN.torch = torch
+    np.savez_compressed(os.path.join(HERE, "sa_loop.npz"), **out)
+
+
 def loop_fixture():
     H = W = 32
     P, N, G = 8, 8, 3
@@ -230,6 +326,11 @@ def loop_fixture():
 
 
 if __name__ == "__main__":
-    mutate_fixture()
-    loop_fixture()
+    which = sys.argv[1:] or ["mutate", "loop", "sa"]
+    if "mutate" in which:
+        mutate_fixture()
+    if "loop" in which:
+        loop_fixture()
+    if "sa" in which:
+        sa_fixture()
     print("done")

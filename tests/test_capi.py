@@ -102,6 +102,44 @@ REF_SIGS = {
          "min_scale_splats", "max_scale_splats", "k_sigma", "mask_strength", "boost_only",
          "save_video=False", "frame_every=5000", "video_dir=''", "prefix='ga'",
          "loss_png_path=''", "loss_csv_path=''", "loss_log_y=False", "hooks"],
+    ("annealing", "simulated_annealing"):
+        ["target_img_uint8", "H", "W", "device", "n_splats", "mutpb", "mut_sigma_max",
+         "mut_sigma_min", "sigma_schedule", "min_scale_splats", "max_scale_splats", "k_sigma",
+         "mask_strength", "boost_only", "iterations", "temp0", "temp_schedule", "tries_per_iter=1",
+         "save_video=False", "frame_every=10000", "video_dir=''", "prefix='sa'",
+         "loss_png_path=''", "loss_csv_path=''", "loss_log_y=False", "hooks"],
+    ("resize", "choose_work_size"): ["Ht", "Wt", "max_side=128"],
+    ("resize", "scale_genome_pixels_anisotropic"): ["ind", "sH", "sW"],
+    # dtype: numpy's float32 stands in for torch.float32 (no torch in the product path)
+    ("population", "sample_log_scales_beta_linear"):
+        ["B", "N", "s_lo", "s_hi", "m=0.5", "concentration=8.0", "device='cuda'",
+         "dtype=<class 'numpy.float32'>"],
+    ("population", "new_population"):
+        ["batch_size", "n_splats", "H", "W", "min_scale_splats", "max_scale_splats",
+         "device='cuda'", "dtype=<class 'numpy.float32'>"],
+    ("population", "new_individual"):
+        ["n_splats", "H", "W", "min_scale_splats", "max_scale_splats", "device='cuda'"],
+    ("population", "duplicate_individual"): ["ind"],
+    ("population", "population_to_list"): ["pop_tensor"],
+    ("genetic", "tournament_selection"): ["pop", "fits", "k=2"],
+    ("genetic", "crossover_uniform"): ["a", "b", "p=0.5"],
+    ("genetic", "_ensure_one_true"): ["mask"],
+    ("genetic", "mutate_individual"):
+        ["ind", "is_elite", "gen", "total_gens", "schedule", "mut_sigma_max", "mut_sigma_min",
+         "mutpb", "H", "W", "min_scale_splats", "max_scale_splats"],
+    ("utils", "wrap_angle"): ["theta"],
+    ("utils", "_anneal_factor"): ["gen", "total", "kind"],
+    ("utils", "build_mut_sigma"): ["gen", "total_gens", "kind", "mut_sigma_max", "mut_sigma_min"],
+    ("utils", "clamp_genome"): ["ind", "H", "W", "min_scale_splats", "max_scale_splats"],
+    ("utils", "render_axes_angle_to_img"): ["ind_axes_angle", "Hsnap", "Wsnap", "k_sigma", "device"],
+    ("utils", "save_frame_png"):
+        ["gen", "ind_axes_angle", "pad", "prefix", "video_dir", "H", "W", "k_sigma", "device",
+         "save_video=True"],
+    ("utils", "prewarm_renderer"): ["H", "W", "k_sigma", "device"],
+    ("utils", "save_loss_curve_png"):
+        ["curves", "out_path", "title='GA fitness over generations'", "xlabel='Generation'",
+         "ylabel='MSE'", "log_y=False", "dpi=144"],
+    ("utils", "save_curves_csv"): ["curves", "out_csv_path"],
     ("mask", "compute_importance_mask"):
         ["target_hw3", "H", "W", "edge_scales=(1, 2, 4)", "w_edge=0.7", "w_var=0.3", "gamma=0.7",
          "floor=0.15", "smooth=0", "strength=1.0"],

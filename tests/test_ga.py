@@ -96,6 +96,13 @@ class ReplayDraws:
         r["swap_u"] = 0.0
         return r
 
+    def mutation(self, n, N, mutpb):          # SA: the tries of one iteration
+        muts = [self._mutation_one(N, mutpb) for _ in range(n)]
+        return {k: np.stack([np.asarray(m[k]) for m in muts]) for k in muts[0]}
+
+    def accept(self):                         # annealing.py:142 random.random()
+        return float(self._py(0))
+
     def generation(self, cx, n_off, N, mutpb):
         masks, muts = [], []
         for i, c in enumerate(cx):

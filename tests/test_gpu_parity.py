@@ -206,6 +206,27 @@ def test_fitness_vs_oracle_1024_config():
                                                              weight_mask=mask))
 
 
+def test_render_2048_config_crops_vs_oracle():
+    """configs[4] shape (run_sags.py: 2048^2, 4096 splats, one candidate): the GPU
+    image on three 96x96 crops (centre, corner, edge) vs the oracle rendering just
+    those windows; fused fitness == fitness of the rendered image."""
+    H = W = 2048
+    pop = O.synthetic_population(1, 4096, H, W, seed=41)
+    img = ggs.render(ggs.encode(pop), H, W)[0]
+    for wy, wx in ((976, 976), (0, 0), (1952, 700)):
+        win = (wy, wy + 96, wx, wx + 96)
+        ref = O.render(O.genome_to_renderer_batched(pop), H, W, window=win)[0]
+        np.testing.assert_allclose(img[wy:wy + 96, wx:wx + 96], ref, atol=IMG_TOL, rtol=0,
+                                   err_msg=str(win))
+    rng = np.random.default_rng(8)
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
+    fused = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+    d2 = ((img.astype(np.float64) - tgt) ** 2).sum(-1)
+    ref = (d2 * mask).sum() / (mask.astype(np.float64).sum() + 1e-12)
+    np.testing.assert_allclose(fused[0], ref, rtol=FIT_RTOL)
+
+
 # ---- full-size properties (512^2 / 256 splats / pop 128) -------------------------------------
 @pytest.fixture(scope="module")
 def full_size():

@@ -140,3 +140,12 @@ def test_synthetic_population_ranges():
     s = np.exp(G[..., 2:4].astype(np.float64))
     assert s.min() >= 3.0 - 1e-4 and s.max() <= 51.2 + 1e-3
     assert (G[..., 8] >= 180).all() and (G[..., 5:9] <= 255).all()
+
+
+def test_oracle_window_render_equals_crop_of_full_render():
+    pop = O.synthetic_population(2, 40, 100, 70, seed=3)
+    G = O.genome_to_renderer_batched(pop)
+    full = O.render(G, 100, 70)
+    for win in ((10, 57, 3, 66), (0, 100, 0, 70), (99, 100, 69, 70)):
+        y0, y1, x0, x1 = win
+        np.testing.assert_array_equal(O.render(G, 100, 70, window=win), full[:, y0:y1, x0:x1])

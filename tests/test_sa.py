@@ -1,0 +1,91 @@
+"""Simulated annealing (ggs/annealing.py) against the REFERENCE's
+simulated_annealing (annealing.py:47-190), draw for draw.
+
+tests/golden/make_golden_ga.py ran the reference on CPU for five temperature
+schedules while recording its torch and Python draws, every fitness call and
+the curves.  Replaying those draws:
+* width 1 (sequential, the reference's schedule): every evaluated neighbour is
+  the reference's genome bit for bit, in the same order;
+* batched speculation (width = tries, and adaptive): the same accepted states,
+  best individual and curves — speculative neighbours the reference never
+  evaluated are discarded before they can influence anything.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from ggs import annealing as A
+from test_ga import CFG, MAX_S, MIN_S, ReplayDraws
+
+CASES = ["cos", "exp", "log", "lin", "cau"]
+
+
+def _case(name):
+    d = load_golden("sa_loop.npz")
+    pre = name + "__"
+    c = {k[len(pre):]: d[k] for k in d.files if k.startswith(pre)}
+    c["target"], (c["H"], c["W"], c["N"]) = d["target"], (int(v) for v in d["dims"])
+    return c
+
+
+def _run(c, speculate, evaluate):
+    iters, tries, T0, mutpb, boost = c["cfg"]
+    return A.simulated_annealing(
+        c["target"], c["H"], c["W"], "cuda", n_splats=c["N"], mutpb=float(mutpb),
+        mut_sigma_max=CFG["mut_sigma_max"], mut_sigma_min=CFG["mut_sigma_min"],
+        sigma_schedule=CFG["schedule"], min_scale_splats=MIN_S, max_scale_splats=MAX_S,
+        k_sigma=3.0, mask_strength=0.7, boost_only=bool(boost), iterations=int(iters),
+        temp0=float(T0), temp_schedule=str(c["sched"]), tries_per_iter=int(tries),
+        draws=ReplayDraws(c), evaluate=evaluate, init_individual=c["init"], progress=False,
+        return_state=True, speculate=speculate)
+
+
+def _check_result(c, out):
+    best, best_fit, st = out
+    np.testing.assert_array_equal(best, c["best"])
+    assert best_fit == float(c["best_fit"])
+    for key in ("best", "current"):
+        np.testing.assert_array_equal(np.asarray(st["curves"][key]), c[f"curve__{key}"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_sa_sequential_matches_reference(name):
+    c = _case(name)
+    calls = []
+
+    def evaluate(G):
+        i = len(calls)
+        assert len(G) == 1
+        np.testing.assert_array_equal(G[0], c[f"call{i}__pop"][0], err_msg=f"call {i}")
+        calls.append(i)
+        return c[f"call{i}__fit"].astype(np.float32)
+
+    out = _run(c, 1, evaluate)
+    assert len(calls) == int(c["n_calls"])
+    _check_result(c, out)
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("speculate", [None, 8])
+def test_sa_batched_speculation_matches_reference(name, speculate):
+    c = _case(name)
+    known = {c[f"call{i}__pop"][0].tobytes(): float(c[f"call{i}__fit"][0])
+             for i in range(int(c["n_calls"]))}
+
+    def evaluate(G):          # neighbours the reference never evaluated get NaN
+        return np.array([known.get(g.tobytes(), np.nan) for g in G], np.float32)
+
+    out = _run(c, speculate, evaluate)
+    _check_result(c, out)
+    st = out[2]["stats"]
+    assert st["evaluated"] >= int(c["n_calls"]) - 1
+
+
+def test_temp_schedules():
+    for kind in ("exp", "linear", "cosine", "log", "cauchy", "other"):
+        vals = [A.temp_schedule(kind, 1e-3, i, 10) for i in range(11)]
+        assert all(v > 0 for v in vals) and vals[0] == pytest.approx(1e-3)
+        assert all(b <= a for a, b in zip(vals, vals[1:]))
+    assert A.temp_schedule("exp", 1.0, 10, 10) == pytest.approx(0.01)

@@ -1,0 +1,58 @@
+"""SA throughput at BASELINE configs[4] (run_sags.py: 2048x2048, 4096 splats,
+SA_TRIES_PER_ITER=8, MUTPB=0.05, T0=1e-3 cosine): iterations/s of
+ggs.annealing.simulated_annealing, sequential tries (speculate=1, the
+reference's one-launch-per-try schedule) vs batched speculation (adaptive).
+
+usage: python tools/bench_sa.py [--iters 20] [--size 2048] [--splats 4096] [--tries 8]"""
+import argparse, json, os, sys, time
+import numpy as np
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "genetic-gaussian-splats_amd"))
+from ggs import annealing as A
+from ggs import ga
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--size", type=int, default=2048)
+ap.add_argument("--splats", type=int, default=4096)
+ap.add_argument("--tries", type=int, default=8)
+ap.add_argument("--mutpb", type=float, default=0.05)
+a = ap.parse_args()
+H = W = a.size
+target = np.random.default_rng(0).uniform(0, 1, (H, W, 3)).astype(np.float32)
+init = ga.new_population(1, a.splats, H, W, 3.0, 0.1, np.random.default_rng(1))[0]
+cfg = dict(mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0, "alpha": 25.0},
+           mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0, "alpha": 2.0})
+from ggs.mask import compute_importance_mask, prepare_target
+from ggs import api
+t = prepare_target(target, H, W)
+m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
+ev = {"s": 0.0}
+
+
+def evaluate(G):
+    t0 = time.perf_counter()
+    f = api.fitness(G, t, H, W, 3.0, weight_mask=m)
+    ev["s"] += time.perf_counter() - t0
+    return f
+
+
+res = {}
+for name, spec in (("sequential", 1), ("speculative", None)):
+    run = lambda n: A.simulated_annealing(          # noqa: E731
+        target, H, W, "cuda", a.splats, a.mutpb, cfg["mut_sigma_max"], cfg["mut_sigma_min"],
+        "cosine", 3.0, 0.1, 3.0, 0.7, False, n, 1e-3, "cosine", a.tries, seed=2,
+        init_individual=init, evaluate=evaluate, progress=False, return_state=True,
+        speculate=spec)
+    run(2)                                           # warm-up
+    ev["s"] = 0.0
+    t0 = time.perf_counter()
+    best, fit, st = run(a.iters)
+    dt = time.perf_counter() - t0
+    res[name] = {"iters_per_s": round(a.iters / dt, 2), "ms_per_iter": round(dt / a.iters * 1e3, 2),
+                 "eval_ms_per_iter": round(ev["s"] / a.iters * 1e3, 2),
+                 "launches": st["stats"]["launches"], "evaluated": st["stats"]["evaluated"],
+                 "best_fit": fit}
+assert res["sequential"]["best_fit"] == res["speculative"]["best_fit"]
+print(json.dumps({"metric": "SA iterations/s", "config": {"H": H, "W": W, "splats": a.splats,
+                  "tries_per_iter": a.tries, "mutpb": a.mutpb, "iters": a.iters}, **res}))
