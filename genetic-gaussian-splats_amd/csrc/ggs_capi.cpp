@@ -694,7 +694,7 @@ GaParamsDev ga_params(const ggs_ga_config& c, int gen, int total) {   // build_m
     float sig[6];
     for (int k = 0; k < 6; ++k)
         sig[k] = (float)(c.sig_min[k] + f * (c.sig_max[k] - c.sig_min[k]));
-    GaParamsDev p;
+    GaParamsDev p{};
     p.sig_xy = sig[0]; p.sig_alog = sig[1]; p.sig_blog = sig[2]; p.sig_theta = sig[3];
     p.sig_rgb = sig[4]; p.sig_alpha = sig[5];
     p.mutpb = c.mutpb; p.cxpb = c.cxpb; p.tour_k = c.tour_k;
@@ -726,8 +726,9 @@ int ga_curves_row(GaSession* s, double** row) {
 }
 
 // Upload one generation's explicit draws into s->draws; returns device views.
-int ga_upload_draws(GaSession* s, const ggs_ga_draws* h, GaDrawsDev* d) {
-    const int64_t P = s->P, N = s->N, K = s->cfg.tour_k, np2 = (P + 1) / 2;
+int ga_upload_draws(DevBuf& buf, hipStream_t st, int64_t P, int64_t N, int64_t K, bool mutation_only,
+                    const ggs_ga_draws* h, GaDrawsDev* d) {
+    const int64_t np2 = (P + 1) / 2;
     struct Seg { const void* src; int64_t bytes; const void** dst; };
     Seg segs[] = {
         {h->tour_idx, 4 * P * K, (const void**)&d->tour_idx}, {h->perm, 4 * P, (const void**)&d->perm},
@@ -741,17 +742,19 @@ int ga_upload_draws(GaSession* s, const ggs_ga_draws* h, GaDrawsDev* d) {
         {h->n_rgba, 16 * P * N, (const void**)&d->n_rgba}, {h->swap_i, 4 * P, (const void**)&d->swap_i},
         {h->swap_pick, 4 * P, (const void**)&d->swap_pick}, {h->swap_u, 8 * P, (const void**)&d->swap_u},
     };
+    const int first = mutation_only ? 4 : 0;   // SA: no selection / crossover draws
     int64_t total = 0;
-    for (const Seg& g : segs) {
-        if (!g.src) return fail(GGS_EINVAL, "ggs_ga_step: every draws array is required");
-        total += (g.bytes + 255) & ~(int64_t)255;
+    for (int k = first; k < (int)(sizeof segs / sizeof segs[0]); ++k) {
+        if (!segs[k].src) return fail(GGS_EINVAL, "every draws array is required");
+        total += (segs[k].bytes + 255) & ~(int64_t)255;
     }
     int rc;
-    if ((rc = ensure(s->draws, (size_t)total, s->st))) return rc;
-    GGS_HIP(hipStreamSynchronize(s->st));   // previous generation may still read the buffer
-    char* base = (char*)s->draws.p;
-    for (const Seg& g : segs) {
-        GGS_HIP(hipMemcpyAsync(base, g.src, (size_t)g.bytes, hipMemcpyHostToDevice, s->st));
+    if ((rc = ensure(buf, (size_t)total, st))) return rc;
+    GGS_HIP(hipStreamSynchronize(st));   // the previous launch may still read the buffer
+    char* base = (char*)buf.p;
+    for (int k = first; k < (int)(sizeof segs / sizeof segs[0]); ++k) {
+        const Seg& g = segs[k];
+        GGS_HIP(hipMemcpyAsync(base, g.src, (size_t)g.bytes, hipMemcpyHostToDevice, st));
         *g.dst = base;
         base += (g.bytes + 255) & ~(int64_t)255;
     }
@@ -761,11 +764,11 @@ int ga_upload_draws(GaSession* s, const ggs_ga_draws* h, GaDrawsDev* d) {
 int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     GaDrawsDev d{};
     int rc;
-    if (hd && (rc = ga_upload_draws(s, hd, &d))) return rc;
+    if (hd && (rc = ga_upload_draws(s->draws, s->st, s->P, s->N, s->cfg.tour_k, false, hd, &d))) return rc;
     const int P = s->P, N = s->N, nxt = 1 - s->cur;
     const GaParamsDev prm = ga_params(s->cfg, gen, total);
     GGS_HIP(launch_ga_variation(s->st, (const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
-                                P, N, prm, d, s->cfg.seed, gen, (float*)s->off.p));
+                                P, N, prm, d, s->cfg.seed, gen, (float*)s->off.p, P));
     if ((rc = run_fitness(s->c, s->st, (const float*)s->off.p, P, N, 9, (const float*)s->target.p,
                           s->mask.p ? (const float*)s->mask.p : nullptr, s->cfg.fitness_mode,
                           s->cfg.boost_beta, s->cfg.H, s->cfg.W, s->cfg.k_sigma, (float*)s->off_fits.p)))
@@ -779,6 +782,49 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     s->cur = nxt;
     s->n_curves += 1;
     return GGS_OK;
+}
+
+struct SaSession {
+    DevCtx* c = nullptr;
+    hipStream_t st = nullptr;
+    ggs_ga_config cfg{};
+    int N = 0, cap = 0, last_n = 0;
+    DevBuf curr, best, nb, nb_fits, target, mask, draws;
+    float* h_fits = nullptr;   // pinned
+};
+
+void sa_free(SaSession* s) {
+    for (DevBuf* b : {&s->curr, &s->best, &s->nb, &s->nb_fits, &s->target, &s->mask, &s->draws})
+        if (b->p) (void)hipFree(b->p);
+    if (s->h_fits) (void)hipHostFree(s->h_fits);
+    if (s->st) (void)hipStreamDestroy(s->st);
+}
+
+int sa_eval(SaSession* s, const float* G, int n, float* dev_out) {
+    return run_fitness(s->c, s->st, G, n, s->N, 9, (const float*)s->target.p,
+                       s->mask.p ? (const float*)s->mask.p : nullptr, s->cfg.fitness_mode,
+                       s->cfg.boost_beta, s->cfg.H, s->cfg.W, s->cfg.k_sigma, dev_out);
+}
+
+// Shared validation of ggs_ga_create / ggs_sa_create.
+int ga_check_config(const ggs_ga_config& c, const float* mask_hw, bool sa) {
+    int rc = check_dims(c.pop_size, c.n_splats, 9, c.H, c.W);
+    if (rc) return rc;
+    if (c.pop_size < 1 || c.pop_size > ga_max_population())
+        return fail(GGS_EINVAL, "pop_size must be in [1, %d]", ga_max_population());
+    if (!sa && c.tour_k < 1) return fail(GGS_EINVAL, "tour_k must be >= 1");
+    if (!sa && c.elite_k > c.pop_size) return fail(GGS_EINVAL, "elite_k must be <= pop_size");
+    if (c.fitness_mode < GGS_FIT_NONE || c.fitness_mode > GGS_FIT_BOOST)
+        return fail(GGS_EINVAL, "bad fitness mode %d", c.fitness_mode);
+    if (c.fitness_mode != GGS_FIT_NONE && !mask_hw) return fail(GGS_EINVAL, "mode needs a mask");
+    return GGS_OK;
+}
+
+void ga_fill_log_bounds(ggs_ga_config* c) {   // utils.py:38-39 when the caller passed 0, 0
+    if (c->scale_log_lo == 0.0f && c->scale_log_hi == 0.0f) {
+        c->scale_log_lo = logf(c->min_scale_splats);
+        c->scale_log_hi = logf(c->max_scale_splats * (float)std::max(c->H, c->W));
+    }
 }
 
 void ga_free(GaSession* s) {
@@ -798,24 +844,14 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
                   const float* mask_hw, const float* init_pop, void** handle) {
     if (!cfg || !target_hw3 || !init_pop || !handle) return fail(GGS_EINVAL, "null argument");
     const ggs_ga_config& c = *cfg;
-    int rc = check_dims(c.pop_size, c.n_splats, 9, c.H, c.W);
+    int rc = ga_check_config(c, mask_hw, false);
     if (rc) return rc;
-    if (c.pop_size < 1 || c.pop_size > ga_max_population())
-        return fail(GGS_EINVAL, "pop_size must be in [1, %d]", ga_max_population());
-    if (c.tour_k < 1) return fail(GGS_EINVAL, "tour_k must be >= 1");
-    if (c.elite_k > c.pop_size) return fail(GGS_EINVAL, "elite_k must be <= pop_size");
-    if (c.fitness_mode < GGS_FIT_NONE || c.fitness_mode > GGS_FIT_BOOST)
-        return fail(GGS_EINVAL, "bad fitness mode %d", c.fitness_mode);
-    if (c.fitness_mode != GGS_FIT_NONE && !mask_hw) return fail(GGS_EINVAL, "mode needs a mask");
     DevCtx* ctx = nullptr;
     if ((rc = get_ctx(device, &ctx))) return rc;
     auto s = std::make_unique<GaSession>();
     s->c = ctx;
     s->cfg = c;
-    if (s->cfg.scale_log_lo == 0.0f && s->cfg.scale_log_hi == 0.0f) {
-        s->cfg.scale_log_lo = logf(c.min_scale_splats);
-        s->cfg.scale_log_hi = logf(c.max_scale_splats * (float)std::max(c.H, c.W));
-    }
+    ga_fill_log_bounds(&s->cfg);
     s->P = c.pop_size;
     s->N = c.n_splats;
     const size_t pb = sizeof(float) * 9 * (size_t)s->P * s->N, hw = (size_t)c.H * c.W;
@@ -904,6 +940,111 @@ void ggs_ga_destroy(void* handle) {
         DeviceGuard dg(s->c->dev);
         if (s->st) (void)hipStreamSynchronize(s->st);
         ga_free(s);
+    }
+    delete s;
+}
+
+// ---- simulated annealing ------------------------------------------------------
+int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_hw3,
+                  const float* mask_hw, const float* init_ind, void** handle, float* init_fit) {
+    if (!cfg || !target_hw3 || !init_ind || !handle) return fail(GGS_EINVAL, "null argument");
+    int rc = ga_check_config(*cfg, mask_hw, true);
+    if (rc) return rc;
+    DevCtx* ctx = nullptr;
+    if ((rc = get_ctx(device, &ctx))) return rc;
+    auto s = std::make_unique<SaSession>();
+    s->c = ctx;
+    s->cfg = *cfg;
+    ga_fill_log_bounds(&s->cfg);
+    s->N = cfg->n_splats;
+    s->cap = cfg->pop_size;
+    const size_t ib = sizeof(float) * 9 * (size_t)s->N, hw = (size_t)cfg->H * cfg->W;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard dg(ctx->dev);
+    auto bail = [&](int code) { sa_free(s.get()); return code; };
+    if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(GGS_EHIP, "stream creation failed"));
+    if ((rc = ensure(s->curr, std::max<size_t>(ib, 4), s->st)) || (rc = ensure(s->best, std::max<size_t>(ib, 4), s->st)) ||
+        (rc = ensure(s->nb, std::max<size_t>(ib * s->cap, 4), s->st)) ||
+        (rc = ensure(s->nb_fits, sizeof(float) * s->cap, s->st)) ||
+        (rc = ensure(s->target, sizeof(float) * 3 * hw, s->st)) ||
+        (mask_hw && (rc = ensure(s->mask, sizeof(float) * hw, s->st))))
+        return bail(rc);
+    if (hipHostMalloc((void**)&s->h_fits, sizeof(float) * s->cap, hipHostMallocDefault) != hipSuccess)
+        return bail(fail(GGS_ENOMEM, "pinned allocation failed"));
+    if (hipMemcpyAsync(s->target.p, target_hw3, sizeof(float) * 3 * hw, hipMemcpyHostToDevice, s->st) ||
+        (mask_hw && hipMemcpyAsync(s->mask.p, mask_hw, sizeof(float) * hw, hipMemcpyHostToDevice, s->st)) ||
+        hipMemcpyAsync(s->curr.p, init_ind, ib, hipMemcpyHostToDevice, s->st) ||
+        hipMemcpyAsync(s->best.p, init_ind, ib, hipMemcpyHostToDevice, s->st))
+        return bail(fail(GGS_EHIP, "upload failed"));
+    if ((rc = sa_eval(s.get(), (const float*)s->curr.p, 1, (float*)s->nb_fits.p))) return bail(rc);
+    if (hipMemcpyAsync(s->h_fits, s->nb_fits.p, sizeof(float), hipMemcpyDeviceToHost, s->st) ||
+        hipStreamSynchronize(s->st))
+        return bail(fail(GGS_EHIP, "initial evaluation failed"));
+    if (init_fit) *init_fit = s->h_fits[0];
+    *handle = s.release();
+    return GGS_OK;
+}
+
+int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_try, int32_t n,
+                   const ggs_ga_draws* draws, float* fits_out) {
+    if (!handle || !fits_out) return fail(GGS_EINVAL, "null argument");
+    SaSession* s = (SaSession*)handle;
+    if (n < 1 || n > s->cap) return fail(GGS_EINVAL, "n=%d outside [1, %d]", n, s->cap);
+    if (first_try < 0) return fail(GGS_EINVAL, "first_try must be >= 0");
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    DeviceGuard dg(s->c->dev);
+    GaDrawsDev d{};
+    int rc;
+    if (draws && (rc = ga_upload_draws(s->draws, s->st, n, s->N, 1, true, draws, &d))) return rc;
+    GaParamsDev prm = ga_params(s->cfg, it, total_iters);
+    prm.mutate_only = 1;
+    prm.o_base = first_try;
+    GGS_HIP(launch_ga_variation(s->st, (const float*)s->curr.p, nullptr, 1, s->N, prm, d, s->cfg.seed, it,
+                                (float*)s->nb.p, n));
+    if ((rc = sa_eval(s, (const float*)s->nb.p, n, (float*)s->nb_fits.p))) return rc;
+    GGS_HIP(hipMemcpyAsync(s->h_fits, s->nb_fits.p, sizeof(float) * n, hipMemcpyDeviceToHost, s->st));
+    GGS_HIP(hipStreamSynchronize(s->st));
+    memcpy(fits_out, s->h_fits, sizeof(float) * n);
+    s->last_n = n;
+    return GGS_OK;
+}
+
+int ggs_sa_commit(void* handle, int32_t j, int32_t update_best) {
+    if (!handle) return fail(GGS_EINVAL, "null handle");
+    SaSession* s = (SaSession*)handle;
+    if (j >= s->last_n) return fail(GGS_EINVAL, "neighbour %d not proposed (last n=%d)", j, s->last_n);
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    DeviceGuard dg(s->c->dev);
+    const size_t ib = sizeof(float) * 9 * (size_t)s->N;
+    if (j >= 0)
+        GGS_HIP(hipMemcpyAsync(s->curr.p, (const char*)s->nb.p + ib * j, ib, hipMemcpyDeviceToDevice, s->st));
+    if (update_best) GGS_HIP(hipMemcpyAsync(s->best.p, s->curr.p, ib, hipMemcpyDeviceToDevice, s->st));
+    return GGS_OK;
+}
+
+int ggs_sa_read(void* handle, float* current, float* best, float* neighbours) {
+    if (!handle) return fail(GGS_EINVAL, "null handle");
+    SaSession* s = (SaSession*)handle;
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    DeviceGuard dg(s->c->dev);
+    const size_t ib = sizeof(float) * 9 * (size_t)s->N;
+    GGS_HIP(hipStreamSynchronize(s->st));
+    if (current) GGS_HIP(hipMemcpy(current, s->curr.p, ib, hipMemcpyDeviceToHost));
+    if (best) GGS_HIP(hipMemcpy(best, s->best.p, ib, hipMemcpyDeviceToHost));
+    if (neighbours && s->last_n > 0)
+        GGS_HIP(hipMemcpy(neighbours, s->nb.p, ib * s->last_n, hipMemcpyDeviceToHost));
+    return GGS_OK;
+}
+
+void ggs_sa_destroy(void* handle) {
+    if (!handle) return;
+    SaSession* s = (SaSession*)handle;
+    {
+        std::lock_guard<std::mutex> lk(s->c->mu);
+        DeviceGuard dg(s->c->dev);
+        if (s->st) (void)hipStreamSynchronize(s->st);
+        sa_free(s);
     }
     delete s;
 }

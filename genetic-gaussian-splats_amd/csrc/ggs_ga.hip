@@ -107,7 +107,12 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
     const int tid = threadIdx.x;
     const Rng rng{k0, k1, (uint32_t)gen};
 
-    if (tid == 0) {
+    const uint32_t og = (uint32_t)(o + prm.o_base);   // Philox identity of this offspring
+    if (tid == 0 && prm.mutate_only) {
+        s_a = 0;                               // annealing.py:122-128: mutate the current state
+        s_b = 0;
+        s_cx = 0;
+    } else if (tid == 0) {
         // parents 2*pair and 2*pair+1 of the (shuffled) tournament winners
         const int qa = d.perm ? d.perm[2 * pair] : 2 * pair;
         const int qb = d.perm ? d.perm[(2 * pair + 1) % P] : (2 * pair + 1) % P;
@@ -132,8 +137,8 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
             ua0 = d.u_ab[(ob + s) * 2]; ua1 = d.u_ab[(ob + s) * 2 + 1];
             ut = d.u_t[ob + s]; urgb = d.u_rgb[ob + s]; ua = d.u_a[ob + s];
         } else {
-            const U4 r1 = rng.block(S_MASK, (uint32_t)o, (uint32_t)(2 * s));
-            const U4 r2 = rng.block(S_MASK, (uint32_t)o, (uint32_t)(2 * s + 1));
+            const U4 r1 = rng.block(S_MASK, og, (uint32_t)(2 * s));
+            const U4 r2 = rng.block(S_MASK, og, (uint32_t)(2 * s + 1));
             ux0 = u01(r1.x); ux1 = u01(r1.y); ua0 = u01(r1.z); ua1 = u01(r1.w);
             ut = u01(r2.x); urgb = u01(r2.y); ua = u01(r2.z);
         }
@@ -148,10 +153,10 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
     any_t = __syncthreads_or(any_t);
     // genetic.py:24-29: fallback flat indices (k into [N,2] or [N,1] row-major)
     int kc = -1, kx = -1, kb = -1, kt = -1;
-    if (!any_color) kc = d.k_color ? d.k_color[o] : (int)(rng.block(S_IND, (uint32_t)o, 0).x % (uint32_t)(2 * N));
-    if (!any_xy) kx = d.k_xy ? d.k_xy[o] : (int)(rng.block(S_IND, (uint32_t)o, 1).x % (uint32_t)(2 * N));
-    if (!any_ab) kb = d.k_ab ? d.k_ab[o] : (int)(rng.block(S_IND, (uint32_t)o, 2).x % (uint32_t)(2 * N));
-    if (!any_t) kt = d.k_t ? d.k_t[o] : (int)(rng.block(S_IND, (uint32_t)o, 3).x % (uint32_t)N);
+    if (!any_color) kc = d.k_color ? d.k_color[o] : (int)(rng.block(S_IND, og, 0).x % (uint32_t)(2 * N));
+    if (!any_xy) kx = d.k_xy ? d.k_xy[o] : (int)(rng.block(S_IND, og, 1).x % (uint32_t)(2 * N));
+    if (!any_ab) kb = d.k_ab ? d.k_ab[o] : (int)(rng.block(S_IND, og, 2).x % (uint32_t)(2 * N));
+    if (!any_t) kt = d.k_t ? d.k_t[o] : (int)(rng.block(S_IND, og, 3).x % (uint32_t)N);
 
     // pass 2: build the child row, mutate, wrap, clamp -> off
     for (int s = tid; s < N; s += VT) {
@@ -168,19 +173,19 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
             nr2 = d.n_rgba[(ob + s) * 4 + 2]; nr3 = d.n_rgba[(ob + s) * 4 + 3];
             if (s_cx) cxu = d.cx_u[(int64_t)pair * N + s];
         } else {
-            const U4 r1 = rng.block(S_MASK, (uint32_t)o, (uint32_t)(2 * s));
-            const U4 r2 = rng.block(S_MASK, (uint32_t)o, (uint32_t)(2 * s + 1));
+            const U4 r1 = rng.block(S_MASK, og, (uint32_t)(2 * s));
+            const U4 r2 = rng.block(S_MASK, og, (uint32_t)(2 * s + 1));
             ux0 = u01(r1.x); ux1 = u01(r1.y); ua0 = u01(r1.z); ua1 = u01(r1.w);
             ut = u01(r2.x); urgb = u01(r2.y); ua = u01(r2.z);
-            const U4 g1 = rng.block(S_NORM_A, (uint32_t)o, (uint32_t)s);
-            const U4 g2 = rng.block(S_NORM_B, (uint32_t)o, (uint32_t)s);
-            const U4 g3 = rng.block(S_NORM_C, (uint32_t)o, (uint32_t)s);
+            const U4 g1 = rng.block(S_NORM_A, og, (uint32_t)s);
+            const U4 g2 = rng.block(S_NORM_B, og, (uint32_t)s);
+            const U4 g3 = rng.block(S_NORM_C, og, (uint32_t)s);
             nx0 = normal_from(g1.x, g1.y); nx1 = normal_from(g1.z, g1.w);
             na0 = normal_from(g2.x, g2.y); na1 = normal_from(g2.z, g2.w);
             nt = normal_from(g3.x, g3.y); nr0 = normal_from(g3.z, g3.w);
-            const U4 g4 = rng.block(S_NORM_C, (uint32_t)o, (uint32_t)(s + N));
+            const U4 g4 = rng.block(S_NORM_C, og, (uint32_t)(s + N));
             nr1 = normal_from(g4.x, g4.y); nr2 = normal_from(g4.z, g4.w);
-            const U4 g5 = rng.block(S_NORM_C, (uint32_t)o, (uint32_t)(s + 2 * N));
+            const U4 g5 = rng.block(S_NORM_C, og, (uint32_t)(s + 2 * N));
             nr3 = normal_from(g5.x, g5.y);
             if (s_cx) cxu = u01(rng.block(S_CX, (uint32_t)pair, (uint32_t)(s + 1)).x);   // shared by the pair
         }
@@ -224,7 +229,7 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
     // genetic.py:79-91: pick i, then the pick-th later splat bigger than i
     int i;
     if (d.swap_i) i = d.swap_i[o];
-    else i = (int)(rng.block(S_IND, (uint32_t)o, 4).x % (uint32_t)(N - 1));
+    else i = (int)(rng.block(S_IND, og, 4).x % (uint32_t)(N - 1));
     if (tid == 0) {
         s_sizei = expf(O[(int64_t)i * 9 + 2]) * expf(O[(int64_t)i * 9 + 3]);
         s_j = -1;
@@ -252,7 +257,7 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
     int pick;
     if (d.swap_pick && d.swap_pick[o] >= 0) pick = d.swap_pick[o];
     else {
-        const double u = d.swap_u ? d.swap_u[o] : (double)u01(rng.block(S_IND, (uint32_t)o, 5).x);
+        const double u = d.swap_u ? d.swap_u[o] : (double)u01(rng.block(S_IND, og, 5).x);
         pick = (int)(u * (double)count);
         if (pick > count - 1) pick = count - 1;
     }
@@ -394,8 +399,8 @@ ga_gather_kernel(const float* __restrict__ pop, const float* __restrict__ off, i
 // ---------------------------------------------------------------------------
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
-                               float* off) {
-    hipLaunchKernelGGL(ga_variation_kernel, dim3(P), dim3(VT), 0, st, pop, fits, P, N, prm, d,
+                               float* off, int n_off) {
+    hipLaunchKernelGGL(ga_variation_kernel, dim3(n_off), dim3(VT), 0, st, pop, fits, P, N, prm, d,
                        (uint32_t)seed, (uint32_t)(seed >> 32), gen, off);
     return hipGetLastError();
 }

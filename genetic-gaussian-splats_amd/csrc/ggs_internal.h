@@ -40,6 +40,8 @@ struct GaParamsDev {            // one generation's operator parameters (float32
     float sig_xy, sig_alog, sig_blog, sig_theta, sig_rgb, sig_alpha;   // build_mut_sigma
     float mutpb, cxpb;
     int tour_k;
+    int mutate_only;            // SA neighbours: every offspring = mutation of pop[0], no selection
+    int o_base;                 // Philox key offset of offspring 0 (SA: index of the first try)
     float log_lo, log_hi;       // clamp_genome scale bounds (utils.py:38-39)
 };
 struct GaDrawsDev {             // explicit draws (device pointers); all NULL -> Philox in-kernel
@@ -64,7 +66,7 @@ struct GaBestDev {
 };
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
-                               float* off);
+                               float* off, int n_off);   // n_off offspring (GA: P; SA: tries)
 hipError_t launch_ga_survivors(hipStream_t st, const float* fits, const float* off_fits, int P,
                                int elite_k, int* src, float* new_fits, const GaBestDev& best,
                                double* curves_row, int init);

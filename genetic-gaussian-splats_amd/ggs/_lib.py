@@ -70,6 +70,13 @@ SIGNATURES = {
     "ggs_ga_run": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "ggs_ga_read": (C.c_int, [C.c_void_p, _f32p, _f32p, _f32p, _f64p, _f64p, _i32p]),
     "ggs_ga_destroy": (None, [C.c_void_p]),
+    "ggs_sa_create": (C.c_int, [C.c_int32, C.POINTER(GaConfig), _f32p, _f32p, _f32p,
+                                C.POINTER(C.c_void_p), _f32p]),
+    "ggs_sa_propose": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                 C.POINTER(GaDraws), _f32p]),
+    "ggs_sa_commit": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "ggs_sa_read": (C.c_int, [C.c_void_p, _f32p, _f32p, _f32p]),
+    "ggs_sa_destroy": (None, [C.c_void_p]),
 }
 
 
@@ -87,7 +94,34 @@ class GGSInputError(AssertionError, ValueError):
     (render.py:219, :223), hence the AssertionError base; ValueError too."""
 
 
+def _share_hip_runtime_with_torch() -> None:
+    """One HIP runtime per process.  PyTorch-ROCm wheels bundle their own
+    libamdhip64 (same SONAME as /opt/rocm's).  If libggs binds /opt/rocm's copy
+    first, a later ``import torch`` loads a second runtime and whichever
+    initialises second finds no GPU.  The reference's callers hand us torch
+    tensors, so when torch is installed (not necessarily imported) its runtime is
+    loaded first (RTLD_GLOBAL) and libggs binds to it by SONAME.
+    GGS_HIP_RUNTIME=system skips this."""
+    if os.environ.get("GGS_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    tlib = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    hip = os.path.join(tlib, "libamdhip64.so")
+    if os.path.exists(hip):
+        for dep in ("libhsa-runtime64.so", "libamdhip64.so"):
+            p = os.path.join(tlib, dep)
+            if os.path.exists(p):
+                C.CDLL(p, mode=C.RTLD_GLOBAL)
+
+
 def _load() -> C.CDLL:
+    _share_hip_runtime_with_torch()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libggs.so not found at {LIB_PATH}: build it with "

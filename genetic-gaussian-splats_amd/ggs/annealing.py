@@ -58,96 +58,116 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
                         loss_log_y: bool = False, *, seed: Optional[int] = None, draws=None,
                         evaluate: Optional[Callable[[np.ndarray], np.ndarray]] = None,
                         init_individual: Optional[np.ndarray] = None, progress: bool = True,
-                        return_state: bool = False, speculate: Optional[int] = None):
+                        return_state: bool = False, speculate: Optional[int] = None,
+                        backend: str = "auto"):
     """annealing.py:47-190 → (best individual [N, 9] float32, best energy).
 
     Keyword-only hooks as ggs.ga.genetic_approx (``seed``, ``draws`` — a source
     with ``mutation(n, N, mutpb)`` and ``accept()`` —, ``evaluate``,
-    ``init_individual``, ``return_state``) plus ``speculate`` (see module doc)."""
+    ``init_individual``, ``return_state``) plus ``speculate`` (see module doc)
+    and ``backend``: "host" (numpy mutation + one libggs launch per batch),
+    "device" (current state resident in HBM, mutation in-kernel: Philox keyed by
+    (seed, iteration, try), or the explicit ``draws``; ggs/ga_device.DeviceSA) or
+    "auto" (device unless an ``evaluate`` hook is given)."""
     from .mask import compute_importance_mask, prepare_target
     sched = temp_schedule
     t = prepare_target(target_img_uint8, H, W)                       # annealing.py:87
     imp_mask = compute_importance_mask(t, H, W, edge_scales=(1, 2, 4), w_edge=0.7, w_var=0.3,
                                        gamma=0.7, floor=0.15, smooth=3,
                                        strength=mask_strength)        # annealing.py:89-94
+    if backend == "auto":
+        backend = "device" if evaluate is None else "host"
     if evaluate is None:
         from . import api
 
         def evaluate(G):
             return api.fitness(G, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only)
+    explicit = draws is not None
     draws = draws if draws is not None else NumpyDraws(seed)
     curr = (np.array(init_individual, np.float32, copy=True) if init_individual is not None else
             new_population(1, n_splats, H, W, min_scale_splats, max_scale_splats,
                            np.random.default_rng(seed))[0])
     N = curr.shape[0]
-    curr_fit = float(np.asarray(evaluate(curr[None]), np.float32)[0])   # annealing.py:99-101
-    best = curr.copy()
-    best_fit = curr_fit
-    curves = {"best": [best_fit], "current": [curr_fit]}
-    pad = len(str(iterations))
-    if save_video:
-        save_frame_png(0, best, pad, prefix, video_dir, H, W, k_sigma, device, save_video)
-
     tries = max(0, int(tries_per_iter))
-    acc_rate = 0.0                     # EWMA of the per-try acceptance rate
-    stats = {"evaluated": 0, "tries": 0, "launches": 0}
-    bar = range(iterations)
-    if progress:
-        try:
-            from tqdm.auto import tqdm
-            bar = tqdm(bar, desc="SA iterations", leave=True)
-        except ImportError:
-            pass
+    if backend == "device":
+        prop = _DeviceProposer(t, imp_mask, curr, max(1, tries), mutpb, mut_sigma_max,
+                               mut_sigma_min, sigma_schedule, min_scale_splats, max_scale_splats,
+                               k_sigma, boost_only, seed)
+    elif backend == "host":
+        prop = _HostProposer(curr, evaluate, iterations, sigma_schedule, mut_sigma_max,
+                             mut_sigma_min, mutpb, H, W, min_scale_splats, max_scale_splats)
+    else:
+        raise ValueError(f"backend must be 'auto', 'host' or 'device', got {backend!r}")
     try:
-        for it in bar:
-            T = sched_T = _T(sched, temp0, it, iterations)
-            accepted_any = False
-            e_curr = float(curr_fit)
-            d = draws.mutation(tries, N, mutpb) if tries else None
-            k = 0
-            while k < tries:
-                if speculate is not None:
-                    w = max(1, int(speculate))
-                else:
-                    w = tries if acc_rate < 1.0 / tries else max(1, int(round(1.0 / acc_rate)))
-                w = min(w, tries - k)
-                nb = mutate_batch(np.repeat(curr[None], w, axis=0), _slice(d, k, k + w), it,
-                                  iterations, sigma_schedule, mut_sigma_max, mut_sigma_min, mutpb,
-                                  H, W, min_scale_splats, max_scale_splats)
-                e = np.asarray(evaluate(nb), np.float32)
-                stats["evaluated"] += w
-                stats["launches"] += 1
-                for j in range(w):
-                    e_new = float(e[j])
-                    dE = e_new - e_curr                                    # annealing.py:133
-                    acc = dE <= 0.0
-                    if not acc and T > 0.0:
-                        acc = draws.accept() < math.exp(-dE / T)           # annealing.py:140-142
-                    k += 1
-                    acc_rate = 0.9 * acc_rate + 0.1 * float(acc)
-                    if acc:
-                        curr = nb[j].copy()
-                        curr_fit = e_new
-                        e_curr = curr_fit
-                        accepted_any = True
-                    if e_curr + 1e-12 < best_fit:                          # annealing.py:148-150
-                        best_fit = e_curr
-                        best = curr.copy()
-                    if acc:
-                        break                  # the rest of the batch came from the old state
-            stats["tries"] += tries
-            curves["best"].append(best_fit)
-            curves["current"].append(float(curr_fit))
-            if save_video and (it + 1) % max(1, frame_every) == 0:
-                save_frame_png(it + 1, best, pad, prefix, video_dir, H, W, k_sigma, device, save_video)
-            if hasattr(bar, "set_postfix"):
-                bar.set_postfix(best_mse=f"{best_fit:.6f}", curr_mse=f"{float(curr_fit):.6f}",
-                                T=f"{sched_T:.4g}", accepted="Y" if accepted_any else "N")
-    except KeyboardInterrupt:
-        print("\n[Interrupted] Returning current best…", flush=True)
+        curr_fit = prop.init_fit                                           # annealing.py:99-101
+        best_fit = curr_fit
+        curves = {"best": [best_fit], "current": [curr_fit]}
+        pad = len(str(iterations))
+        if save_video:
+            save_frame_png(0, prop.best(), pad, prefix, video_dir, H, W, k_sigma, device, save_video)
+
+        acc_rate = 0.0                 # EWMA of the per-try acceptance rate
+        stats = {"evaluated": 0, "tries": 0, "launches": 0}
+        bar = range(iterations)
+        if progress:
+            try:
+                from tqdm.auto import tqdm
+                bar = tqdm(bar, desc="SA iterations", leave=True)
+            except ImportError:
+                pass
+        try:
+            for it in bar:
+                T = _T(sched, temp0, it, iterations)
+                accepted_any = False
+                e_curr = float(curr_fit)
+                d = draws.mutation(tries, N, mutpb) if tries and (explicit or backend == "host") \
+                    else None
+                k = 0
+                while k < tries:
+                    if speculate is not None:
+                        w = max(1, int(speculate))
+                    else:
+                        w = tries if acc_rate < 1.0 / tries else max(1, int(round(1.0 / acc_rate)))
+                    w = min(w, tries - k)
+                    e = prop.propose(it, iterations, k, w, None if d is None else _slice(d, k, k + w))
+                    stats["evaluated"] += w
+                    stats["launches"] += 1
+                    for j in range(w):
+                        e_new = float(e[j])
+                        dE = e_new - e_curr                                # annealing.py:133
+                        acc = dE <= 0.0
+                        if not acc and T > 0.0:
+                            acc = draws.accept() < math.exp(-dE / T)       # annealing.py:140-142
+                        k += 1
+                        acc_rate = 0.9 * acc_rate + 0.1 * float(acc)
+                        if acc:
+                            curr_fit = e_new
+                            e_curr = curr_fit
+                            accepted_any = True
+                        new_best = e_curr + 1e-12 < best_fit               # annealing.py:148-150
+                        if new_best:
+                            best_fit = e_curr
+                        if acc or new_best:
+                            prop.commit(j if acc else -1, new_best)
+                        if acc:
+                            break              # the rest of the batch came from the old state
+                stats["tries"] += tries
+                curves["best"].append(best_fit)
+                curves["current"].append(float(curr_fit))
+                if save_video and (it + 1) % max(1, frame_every) == 0:
+                    save_frame_png(it + 1, prop.best(), pad, prefix, video_dir, H, W, k_sigma,
+                                   device, save_video)
+                if hasattr(bar, "set_postfix"):
+                    bar.set_postfix(best_mse=f"{best_fit:.6f}", curr_mse=f"{float(curr_fit):.6f}",
+                                    T=f"{T:.4g}", accepted="Y" if accepted_any else "N")
+        except KeyboardInterrupt:
+            print("\n[Interrupted] Returning current best…", flush=True)
+        finally:
+            if hasattr(bar, "close"):
+                bar.close()
+        best, curr = prop.best(), prop.current()
     finally:
-        if hasattr(bar, "close"):
-            bar.close()
+        prop.close()
 
     try:                                                                   # annealing.py:174-188
         save_loss_curve_png(curves, loss_png_path, title=f"{prefix} energy (MSE)",
@@ -166,3 +186,65 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
 
 
 _T = temp_schedule
+
+
+class _HostProposer:
+    """Neighbours mutated by ggs.ga.mutate_batch, evaluated by ``evaluate``."""
+
+    def __init__(self, curr, evaluate, iterations, schedule, sig_max, sig_min, mutpb, H, W,
+                 min_s, max_s):
+        self.curr, self.evaluate = curr, evaluate
+        self.args = (iterations, schedule, sig_max, sig_min, mutpb, H, W, min_s, max_s)
+        self.init_fit = float(np.asarray(evaluate(curr[None]), np.float32)[0])
+        self._best = curr.copy()
+        self.nb = None
+
+    def propose(self, it, total, first_try, w, d):
+        total_, sched, smax, smin, mutpb, H, W, lo, hi = self.args
+        self.nb = mutate_batch(np.repeat(self.curr[None], w, axis=0), d, it, total_, sched, smax,
+                               smin, mutpb, H, W, lo, hi)
+        return np.asarray(self.evaluate(self.nb), np.float32)
+
+    def commit(self, j, update_best):
+        if j >= 0:
+            self.curr = self.nb[j].copy()
+        if update_best:
+            self._best = self.curr.copy()
+
+    def best(self):
+        return self._best.copy()
+
+    def current(self):
+        return self.curr.copy()
+
+    def close(self):
+        pass
+
+
+class _DeviceProposer:
+    """Neighbours mutated and evaluated on the GPU (ggs_sa_*)."""
+
+    def __init__(self, t, mask, curr, max_tries, mutpb, sig_max, sig_min, schedule, min_s, max_s,
+                 k_sigma, boost_only, seed):
+        from .ga_device import DeviceSA
+        self.sa = DeviceSA(t, mask, curr, max_tries=max_tries, mutpb=mutpb, mut_sigma_max=sig_max,
+                           mut_sigma_min=sig_min, schedule=schedule, min_scale_splats=min_s,
+                           max_scale_splats=max_s, k_sigma=k_sigma, boost_only=boost_only,
+                           seed=(int(np.random.SeedSequence().entropy) if seed is None
+                                 else int(seed)) & (2**64 - 1))
+        self.init_fit = float(self.sa.init_fit)
+
+    def propose(self, it, total, first_try, w, d):
+        return self.sa.propose(it, total, first_try, w, d)
+
+    def commit(self, j, update_best):
+        self.sa.commit(j, update_best)
+
+    def best(self):
+        return self.sa.read()[1]
+
+    def current(self):
+        return self.sa.read()[0]
+
+    def close(self):
+        self.sa.close()

@@ -28,6 +28,95 @@ def _arr(x, dt):
     return np.ascontiguousarray(x, dtype=dt)
 
 
+def _config(P, N, H, W, tour_k, elite_k, cxpb, mutpb, k_sigma, min_scale_splats,
+            max_scale_splats, mask, boost_only, boost_beta, schedule, mut_sigma_max,
+            mut_sigma_min, seed) -> GaConfig:
+    from .ga import scale_log_bounds
+    lo, hi = scale_log_bounds(H, W, min_scale_splats, max_scale_splats)
+    mode = (_lib.GGS_FIT_NONE if mask is None else
+            _lib.GGS_FIT_BOOST if boost_only else _lib.GGS_FIT_WEIGHTED)
+    return GaConfig(P, N, H, W, tour_k, elite_k, cxpb, mutpb, k_sigma, min_scale_splats,
+                    max_scale_splats, float(lo), float(hi), mode, boost_beta,
+                    SCHEDULES.get(schedule, 0),
+                    (C.c_double * 6)(*[mut_sigma_max[k] for k in SIG_KEYS]),
+                    (C.c_double * 6)(*[mut_sigma_min[k] for k in SIG_KEYS]), seed & (2**64 - 1))
+
+
+def _draws_struct(draws, keep, fields=None) -> GaDraws:
+    d = GaDraws()
+    for name, typ in GaDraws._fields_:
+        if fields is not None and name not in fields:
+            continue
+        dt = np.float64 if name == "swap_u" else (np.int32 if typ is _i32p else np.float32)
+        a = keep[name] = _arr(draws[name], dt)
+        setattr(d, name, a.ctypes.data_as(typ))
+    return d
+
+
+MUTATION_KEYS = ("u_xy", "u_ab", "u_t", "u_rgb", "u_a", "k_color", "k_xy", "k_ab", "k_t", "n_xy",
+                 "n_ab", "n_t", "n_rgba", "swap_i", "swap_pick", "swap_u")
+
+
+class DeviceSA:
+    """Device-resident SA state (ggs_sa_* in include/ggs.h): the current and best
+    individuals live in HBM; ``propose`` returns the energies of a batch of tries."""
+
+    def __init__(self, target, mask, init_ind, *, max_tries: int, mutpb: float,
+                 mut_sigma_max: Dict[str, float], mut_sigma_min: Dict[str, float],
+                 schedule: str, min_scale_splats: float, max_scale_splats: float,
+                 k_sigma: float = 3.0, boost_only: bool = False, boost_beta: float = 1.0,
+                 seed: int = 0, device: int = 0):
+        ind = _arr(init_ind, np.float32)
+        if ind.ndim != 2 or ind.shape[1] != 9:
+            raise _lib.GGSInputError("the device SA keeps an [N, 9] genome")
+        self.target = _arr(target, np.float32)
+        H, W = self.target.shape[:2]
+        self.mask = None if mask is None else _arr(mask, np.float32)
+        self.N, self.cap = ind.shape[0], max(1, int(max_tries))
+        cfg = _config(self.cap, self.N, H, W, 1, 0, 0.0, mutpb, k_sigma, min_scale_splats,
+                      max_scale_splats, self.mask, boost_only, boost_beta, schedule,
+                      mut_sigma_max, mut_sigma_min, seed)
+        _lib.ensure_init()
+        h = C.c_void_p()
+        f = C.c_float()
+        check(lib.ggs_sa_create(device, C.byref(cfg), self.target.ctypes.data_as(_f32p),
+                                None if self.mask is None else self.mask.ctypes.data_as(_f32p),
+                                ind.ctypes.data_as(_f32p), C.byref(h), C.byref(f)),
+              "ggs_sa_create")
+        self.h, self.init_fit, self.last_n = h, f.value, 0
+
+    def propose(self, it: int, total: int, first_try: int, n: int, draws=None) -> np.ndarray:
+        out = np.empty(n, np.float32)
+        keep = {}
+        d = None if draws is None else C.byref(_draws_struct(draws, keep, MUTATION_KEYS))
+        check(lib.ggs_sa_propose(self.h, it, total, first_try, n, d, out.ctypes.data_as(_f32p)),
+              "ggs_sa_propose")
+        self.last_n = n
+        return out
+
+    def commit(self, j: int, update_best: bool) -> None:
+        check(lib.ggs_sa_commit(self.h, j, int(bool(update_best))), "ggs_sa_commit")
+
+    def read(self):
+        cur = np.empty((self.N, 9), np.float32)
+        best = np.empty((self.N, 9), np.float32)
+        nb = np.empty((max(self.last_n, 1), self.N, 9), np.float32)
+        check(lib.ggs_sa_read(self.h, cur.ctypes.data_as(_f32p), best.ctypes.data_as(_f32p),
+                              nb.ctypes.data_as(_f32p)), "ggs_sa_read")
+        return cur, best, nb[:self.last_n]
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib.ggs_sa_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 — interpreter shutdown
+            pass
+
+
 class DeviceGA:
     """One device-resident GA population (see module docstring)."""
 
@@ -36,7 +125,6 @@ class DeviceGA:
                  schedule: str, min_scale_splats: float, max_scale_splats: float,
                  k_sigma: float = 3.0, boost_only: bool = False, boost_beta: float = 1.0,
                  seed: int = 0, device: int = 0):
-        from .ga import scale_log_bounds
         pop = _arr(init_pop, np.float32)
         P, N, Cc = pop.shape
         if Cc != 9:
@@ -44,14 +132,9 @@ class DeviceGA:
         self.target = _arr(target, np.float32)
         H, W = self.target.shape[:2]
         self.mask = None if mask is None else _arr(mask, np.float32)
-        lo, hi = scale_log_bounds(H, W, min_scale_splats, max_scale_splats)
-        cfg = GaConfig(P, N, H, W, tour_k, elite_k, cxpb, mutpb, k_sigma, min_scale_splats,
-                       max_scale_splats, float(lo), float(hi),
-                       _lib.GGS_FIT_NONE if self.mask is None else
-                       (_lib.GGS_FIT_BOOST if boost_only else _lib.GGS_FIT_WEIGHTED),
-                       boost_beta, SCHEDULES.get(schedule, 0),
-                       (C.c_double * 6)(*[mut_sigma_max[k] for k in SIG_KEYS]),
-                       (C.c_double * 6)(*[mut_sigma_min[k] for k in SIG_KEYS]), seed & (2**64 - 1))
+        cfg = _config(P, N, H, W, tour_k, elite_k, cxpb, mutpb, k_sigma, min_scale_splats,
+                      max_scale_splats, self.mask, boost_only, boost_beta, schedule,
+                      mut_sigma_max, mut_sigma_min, seed)
         self.P, self.N, self.H, self.W, self.tour_k, self.cxpb = P, N, H, W, tour_k, cxpb
         _lib.ensure_init()
         h = C.c_void_p()
@@ -66,11 +149,7 @@ class DeviceGA:
             check(lib.ggs_ga_step(self.h, gen, total, None), "ggs_ga_step")
             return
         keep = {}
-        d = GaDraws()
-        for name, typ in GaDraws._fields_:
-            dt = np.float64 if name == "swap_u" else (np.int32 if typ is _i32p else np.float32)
-            a = keep[name] = _arr(draws[name], dt)
-            setattr(d, name, a.ctypes.data_as(typ))
+        d = _draws_struct(draws, keep)
         check(lib.ggs_ga_step(self.h, gen, total, C.byref(d)), "ggs_ga_step")
 
     def run(self, first_gen: int, n_gens: int, total: int) -> None:
@@ -110,9 +189,7 @@ def draws_from_host(tour_idx, perm, cx, cxu_compact, mut, N: int) -> Dict[str, n
     cx_u = np.ones((npairs, N), np.float32)
     cx_u[np.asarray(cx, bool)] = np.asarray(cxu_compact, np.float32).reshape(-1, N)
     out = {"tour_idx": tour_idx, "perm": perm, "cx": np.asarray(cx, np.int32), "cx_u": cx_u}
-    out.update({k: mut[k] for k in ("u_xy", "u_ab", "u_t", "u_rgb", "u_a", "k_color", "k_xy",
-                                    "k_ab", "k_t", "n_xy", "n_ab", "n_t", "n_rgba", "swap_i",
-                                    "swap_pick", "swap_u")})
+    out.update({k: mut[k] for k in MUTATION_KEYS})
     return out
 
 

@@ -158,6 +158,26 @@ int ggs_ga_read(void* handle, float* pop, float* fits, float* best_ind, double* 
                 double* curves, int32_t* n_curves);
 void ggs_ga_destroy(void* handle);
 
+/* ---- device-resident simulated-annealing neighbours (annealing.py:121-150) ---
+ * The current state stays on the GPU.  ggs_sa_propose mutates it into n
+ * neighbours — tries first_try .. first_try+n-1 of iteration `it`, draws either
+ * explicit (ggs_ga_draws layout, mutation fields only, indexed by local try) or
+ * Philox keyed by (seed, it, try), so a try's neighbour does not depend on how
+ * the tries are batched — evaluates them in one launch and returns their
+ * energies.  The host runs the acceptance test (annealing.py:133-146) and
+ * ggs_sa_commit installs the accepted neighbour j (and/or snapshots the best).
+ * cfg: pop_size = the largest n per propose call; tour_k/elite_k/cxpb unused.
+ * Replaces: annealing.py:122-131 (duplicate + mutate_individual + fitness). */
+int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_hw3,
+                  const float* mask_hw, const float* init_ind, void** handle, float* init_fit);
+int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_try, int32_t n,
+                   const ggs_ga_draws* draws, float* fits_out);
+/* j >= 0: current <- neighbour j of the last propose; update_best: best <- current. */
+int ggs_sa_commit(void* handle, int32_t j, int32_t update_best);
+/* Synchronises; any output may be NULL.  neighbours: [n of the last propose][N][9]. */
+int ggs_sa_read(void* handle, float* current, float* best, float* neighbours);
+void ggs_sa_destroy(void* handle);
+
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------
  * When enabled, every launch of "prep", "raster" and "finalize" is bracketed
  * by hipEvents; ggs_profile_read synchronises those events and returns the

@@ -128,20 +128,23 @@ def test_run_ggs_flow_on_gpu(tmp_path):
 def test_config4_sa_speculation_equals_sequential_on_gpu():
     """configs[4] shape: 2048^2, 4096 splats, 8 tries per iteration."""
     from ggs import annealing as A
+    from ggs import ga
     H = W = 2048
     target = np.random.default_rng(3).uniform(0, 1, (H, W, 3)).astype(np.float32)
     init = O.synthetic_population(1, 4096, H, W, seed=5)[0]
     outs = []
-    for spec in (1, None):
+    for spec, backend in ((1, "host"), (None, "host"), (None, "device")):
         outs.append(A.simulated_annealing(
             target, H, W, "cuda", n_splats=4096, mutpb=0.05, mut_sigma_max=CFG["mut_sigma_max"],
             mut_sigma_min=CFG["mut_sigma_min"], sigma_schedule="cosine", min_scale_splats=MIN_S,
             max_scale_splats=MAX_S, k_sigma=3.0, mask_strength=0.7, boost_only=False,
-            iterations=3, temp0=1e-3, temp_schedule="cosine", tries_per_iter=8, seed=9,
-            init_individual=init, progress=False, return_state=True, speculate=spec))
-    (b1, f1, s1), (b2, f2, s2) = outs
+            iterations=3, temp0=1e-3, temp_schedule="cosine", tries_per_iter=8,
+            init_individual=init, progress=False, return_state=True, speculate=spec,
+            backend=backend, draws=ga.NumpyDraws(9)))
+    (b1, f1, s1), (b2, f2, s2), (b3, f3, s3) = outs
     np.testing.assert_array_equal(b1, b2)
-    assert f1 == f2 and s1["curves"] == s2["curves"]
+    np.testing.assert_array_equal(b1, b3)
+    assert f1 == f2 == f3 and s1["curves"] == s2["curves"] == s3["curves"]
     assert s1["stats"]["launches"] == 24 and s2["stats"]["launches"] <= 24
     assert s2["stats"]["evaluated"] >= 24
     c = s1["curves"]["best"]

@@ -144,3 +144,60 @@ def test_device_ga_rejects_bad_config():
     with pytest.raises(AssertionError):
         DeviceGA(t, m, init, tour_k=2, elite_k=5, cxpb=0.5, mutpb=0.1, min_scale_splats=MIN_S,
                  max_scale_splats=MAX_S, **CFG)
+
+
+# ---- device-resident SA neighbours (ggs_sa_*) -------------------------------------------------
+def _sa(target, H, W, N, **kw):
+    from ggs import annealing as A
+    base = dict(mutpb=0.2, mut_sigma_max=CFG["mut_sigma_max"], mut_sigma_min=CFG["mut_sigma_min"],
+                sigma_schedule="cosine", min_scale_splats=MIN_S, max_scale_splats=MAX_S,
+                k_sigma=3.0, mask_strength=0.7, boost_only=False, iterations=6, temp0=2e-3,
+                temp_schedule="cosine", tries_per_iter=4, progress=False, return_state=True)
+    base.update(kw)
+    return A.simulated_annealing(target, H, W, "cuda", n_splats=N, **base)
+
+
+@pytest.mark.parametrize("H,W,N,tries,boost,spec", [(40, 40, 17, 4, False, None),
+                                                     (64, 48, 300, 3, True, 1),
+                                                     (32, 32, 1, 5, False, 5),
+                                                     (48, 48, 2, 8, False, None)])
+def test_device_sa_matches_host_sa_with_same_draws(H, W, N, tries, boost, spec):
+    target, _, _ = _problem(H, W, 5)
+    init = ga.new_population(1, N, H, W, MIN_S, MAX_S, np.random.default_rng(N))[0]
+    kw = dict(tries_per_iter=tries, boost_only=boost, speculate=spec, init_individual=init)
+    hb, hf, hs = _sa(target, H, W, N, backend="host", seed=3, **kw)
+    db, df, ds = _sa(target, H, W, N, backend="device", draws=ga.NumpyDraws(3), **kw)
+    np.testing.assert_array_equal(db, hb)
+    np.testing.assert_array_equal(ds["current"], hs["current"])
+    assert df == hf and ds["curves"] == hs["curves"] and ds["stats"] == hs["stats"]
+
+
+def test_device_sa_replays_reference_draws():
+    from test_ga import ReplayDraws
+    from test_sa import _case
+    for name in ("cos", "exp", "log", "lin", "cau"):
+        c = _case(name)
+        iters, tries, T0, mutpb, boost = c["cfg"]
+        b, f, st = _sa(c["target"], c["H"], c["W"], c["N"], mutpb=float(mutpb),
+                       boost_only=bool(boost), iterations=int(iters), temp0=float(T0),
+                       temp_schedule=str(c["sched"]), tries_per_iter=int(tries),
+                       draws=ReplayDraws(c), init_individual=c["init"], backend="device")
+        np.testing.assert_array_equal(b, c["best"], err_msg=name)
+        assert f == pytest.approx(float(c["best_fit"]), rel=1e-5)
+        for key in ("best", "current"):
+            np.testing.assert_allclose(st["curves"][key], c[f"curve__{key}"], rtol=1e-5)
+
+
+def test_device_sa_philox_width_invariant_and_improves():
+    H = W = 96
+    target, t, m = _problem(H, W, 6)
+    init = ga.new_population(1, 64, H, W, MIN_S, MAX_S, np.random.default_rng(0))[0]
+    outs = [_sa(target, H, W, 64, backend="device", seed=21, speculate=s, iterations=25,
+                tries_per_iter=8, temp0=1e-4, init_individual=init) for s in (1, 3, None)]
+    for b, f, st in outs[1:]:
+        np.testing.assert_array_equal(b, outs[0][0])
+        assert f == outs[0][1] and st["curves"] == outs[0][2]["curves"]
+    b, f, st = outs[0]
+    c = st["curves"]["best"]
+    assert c[-1] < c[0] and all(y <= x for x, y in zip(c, c[1:]))
+    assert float(ggs.fitness(b[None], t, H, W, 3.0, weight_mask=m)[0]) == f

@@ -30,6 +30,21 @@ def _render_cases():
     return sorted(os.path.basename(p)[7:-4] for p in glob.glob(os.path.join(GOLDEN, "render_*.npz")))
 
 
+def test_shares_one_hip_runtime_with_torch():
+    """libggs first, torch second (a fresh process): both see the GPU, because
+    ggs/_lib.py binds libggs to torch's bundled HIP runtime (one runtime per
+    process; two copies fight over the device)."""
+    import subprocess
+    import sys
+    code = ("import numpy as np, ggs; t = np.zeros((8, 8, 3), np.float32); "
+            "g = np.zeros((1, 1, 9), np.float32); print(ggs.fitness(g, t, 8, 8)); "
+            "import torch; print(torch.zeros(1).cuda().device)")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "PYTHONPATH": os.pathsep.join(sys.path)})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "cuda:0" in r.stdout
+
+
 def test_device_present_and_library_native():
     n = ggs.ensure_init()
     assert n >= 1

@@ -1,7 +1,12 @@
 """SA throughput at BASELINE configs[4] (run_sags.py: 2048x2048, 4096 splats,
 SA_TRIES_PER_ITER=8, MUTPB=0.05, T0=1e-3 cosine): iterations/s of
-ggs.annealing.simulated_annealing, sequential tries (speculate=1, the
-reference's one-launch-per-try schedule) vs batched speculation (adaptive).
+ggs.annealing.simulated_annealing over the SA loop alone (setup — target prep,
+importance mask, initial evaluation — is timed separately and subtracted):
+* host / sequential: numpy mutation, one host-API launch per try (the
+  reference's schedule);
+* host / speculative: numpy mutation, batched tries;
+* device / speculative: state resident in HBM, in-kernel mutation (Philox),
+  batched tries, one 4-byte-per-try readback per batch.
 
 usage: python tools/bench_sa.py [--iters 20] [--size 2048] [--splats 4096] [--tries 8]"""
 import argparse, json, os, sys, time
@@ -38,21 +43,26 @@ def evaluate(G):
 
 
 res = {}
-for name, spec in (("sequential", 1), ("speculative", None)):
+for name, spec, backend in (("host_sequential", 1, "host"), ("host_speculative", None, "host"),
+                            ("device_speculative", None, "device")):
     run = lambda n: A.simulated_annealing(          # noqa: E731
         target, H, W, "cuda", a.splats, a.mutpb, cfg["mut_sigma_max"], cfg["mut_sigma_min"],
         "cosine", 3.0, 0.1, 3.0, 0.7, False, n, 1e-3, "cosine", a.tries, seed=2,
-        init_individual=init, evaluate=evaluate, progress=False, return_state=True,
-        speculate=spec)
+        init_individual=init, evaluate=evaluate if backend == "host" else None, progress=False,
+        return_state=True, speculate=spec, backend=backend)
     run(2)                                           # warm-up
+    t0 = time.perf_counter()
+    run(0)                                           # setup only
+    t_setup = time.perf_counter() - t0
     ev["s"] = 0.0
     t0 = time.perf_counter()
     best, fit, st = run(a.iters)
-    dt = time.perf_counter() - t0
+    dt = time.perf_counter() - t0 - t_setup
     res[name] = {"iters_per_s": round(a.iters / dt, 2), "ms_per_iter": round(dt / a.iters * 1e3, 2),
-                 "eval_ms_per_iter": round(ev["s"] / a.iters * 1e3, 2),
+                 "setup_ms": round(t_setup * 1e3, 1),
+                 "eval_ms_per_iter": round(ev["s"] / a.iters * 1e3, 2) if backend == "host" else None,
                  "launches": st["stats"]["launches"], "evaluated": st["stats"]["evaluated"],
                  "best_fit": fit}
-assert res["sequential"]["best_fit"] == res["speculative"]["best_fit"]
+assert res["host_sequential"]["best_fit"] == res["host_speculative"]["best_fit"]
 print(json.dumps({"metric": "SA iterations/s", "config": {"H": H, "W": W, "splats": a.splats,
                   "tries_per_iter": a.tries, "mutpb": a.mutpb, "iters": a.iters}, **res}))
