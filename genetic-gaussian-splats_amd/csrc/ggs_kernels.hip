@@ -110,7 +110,11 @@ __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
     r.r = p.rc;
     r.g = p.gc;
     r.b = p.bc;
-    r.pad0 = r.pad1 = r.pad2 = 0.0f;
+    // f(qy + 8) = f(qy) * 2^d(qy),  d(qy) = e(qy + 8) - e(qy) = 16 Cc qy + 64 Cc + 8 bx,
+    // d(qy + 8) = d(qy) + 128 Cc  ->  the raster walks rows with two multiplies.
+    r.rho = __builtin_amdgcn_exp2f(128.0f * r.Cc);
+    r.c16 = 16.0f * r.Cc;
+    r.c64 = 64.0f * r.Cc;
     r.x0 = p.x0;
     r.x1 = p.x1;
     r.y0 = p.y0;
@@ -176,7 +180,8 @@ __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirst
 //   C += T*f*c ; T *= (1 - f)       (== render.py:194-196 run back-to-front)
 // MASKED adds the per-lane row test for the AABB's first/last row block.
 // Performance-ablation switch (tools/ablate.py; 0 in every shipped build):
-// 1 = exp replaced by a multiply, 2 = no row-group bodies, 3 = red channel only.
+// 1 = exp replaced by a multiply, 2 = no row-group bodies, 3 = red channel only,
+// 4 = cull + epilogue only (no per-splat work).
 #ifndef GGS_ABL
 #define GGS_ABL 0
 #endif
@@ -219,6 +224,16 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
         f_.x = GGS_EXP2(e_.x);                                                       \
         f_.y = GGS_EXP2(e_.y);                                                       \
         const f2_t w_ = P_T##k * f_;                                                 \
+        P_R##k = fma2(w_, cr2, P_R##k);                                              \
+        if (GGS_ABL != 3) P_G##k = fma2(w_, cg2, P_G##k);                            \
+        if (GGS_ABL != 3) P_B##k = fma2(w_, cb2, P_B##k);                            \
+        P_T##k = P_T##k - w_;                                                        \
+    } while (0)
+// Blend one packed pair with given (row-masked) Gaussian values f.
+#define GGS_BLEND(k, F)                                                              \
+    do {                                                                             \
+        if (GGS_ABL == 2) break;                                                     \
+        const f2_t w_ = P_T##k * (F);                                                \
         P_R##k = fma2(w_, cr2, P_R##k);                                              \
         if (GGS_ABL != 3) P_G##k = fma2(w_, cg2, P_G##k);                            \
         if (GGS_ABL != 3) P_B##k = fma2(w_, cb2, P_B##k);                            \
@@ -275,19 +290,22 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
 
+    // bounds of the next 64 splats are loaded one chunk ahead (latency overlap)
+    int4 bbn = *reinterpret_cast<const int4*>(&crec[max(N - 1 - lane, 0)].x0);
     for (int base = 0; base < N; base += 64) {
-        // --- cull 64 splats (descending index = front-to-back) against the strip
+        // --- cull 64 splats (descending index = front-to-back) against the strip:
+        // one 16-B load per lane (clamped index, no short-circuit: a branchy test
+        // splits it into two dependent loads), then a branch-free overlap test
         const int i = N - 1 - (base + lane);
-        bool hit = false;
-        if (i >= 0) {
-            const int4 bb = *reinterpret_cast<const int4*>(&crec[i].x0);   // x0 x1 y0 y1
-            hit = !(bb.w < ty0 || bb.z > ty1 || bb.y < sx0 || bb.x > sx0 + 15);
-        }
+        const int4 bb = bbn;                                                  // x0 x1 y0 y1
+        bbn = *reinterpret_cast<const int4*>(&crec[max(i - 64, 0)].x0);
+        const bool hit = (i >= 0) & (bb.w >= ty0) & (bb.z <= ty1) & (bb.y >= sx0) & (bb.x <= sx0 + 15);
         const uint64_t m = __ballot(hit);
         if (hit) list[cnt + __popcll(m & lt_mask)] = i;
         cnt += __popcll(m);
         if (cnt <= CAP - 64 && base + 64 < N) continue;
         if (cnt == 0) continue;
+        if (GGS_ABL == 4) { asm volatile("" :: "v"(list[lane])); cnt = 0; continue; }
 
         // --- blend the list: splat params arrive in SGPRs (s_load), the next
         //     record is fetched while the current one is blended; list indices
@@ -316,20 +334,75 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             const f2_t qyv = {qy0, qy0 + 4.0f}, Cc2 = Cc, bx2 = bx, px2 = px;
             const f2_t cr2 = cr, cg2 = cg, cb2 = cb;
             const int kA = gA >> 1, kB = gB >> 1;             // first / last group pair
+            f2_t F2, R2;                                       // row recurrence: f, ratio
+            // First pair: exact exponent; keeps the unmasked f as the recurrence
+            // seed and, when more pairs follow, the ratio 2^d to the next pair.
+            // A seed below 2^-100 on a live lane (tiny corner of a thin rotated
+            // splat) would lose the recurrence's precision: that wave walks this
+            // splat with the exact exponent instead (wave-uniform, ~0.3 % of walks).
             switch (kA) {
-#define GGS_FIRST(k) \
-    case k: if (k < NPK) { GGS_PK(k, true); if (kB == k) goto done; goto u##k; } break;
+#define GGS_FIRST(k)                                                                    \
+    case k:                                                                             \
+        if (k < NPK) {                                                                  \
+            const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                  \
+            const f2_t e_ = fma2(qy_, fma2(Cc2, qy_, bx2), px2);                        \
+            F2.x = GGS_EXP2(e_.x);                                                      \
+            F2.y = GGS_EXP2(e_.y);                                                      \
+            f2_t fu_ = F2;                                                              \
+            if ((unsigned)(8 * (k) - rlo) > rspan) fu_.x = 0.0f;                        \
+            if ((unsigned)(8 * (k) + 4 - rlo) > rspan) fu_.y = 0.0f;                    \
+            GGS_BLEND(k, fu_);                                                          \
+            if (kB == k) goto done;                                                     \
+            if (__ballot(inx && fminf(e_.x, e_.y) < -100.0f)) goto x##k;                \
+            const float t8_ = __builtin_fmaf(bx, 8.0f, s.c64);                          \
+            f2_t d_ = fma2(qy_, (f2_t)s.c16, (f2_t)t8_);                                \
+            R2.x = GGS_EXP2(fminf(d_.x, 100.0f));                                       \
+            R2.y = GGS_EXP2(fminf(d_.y, 100.0f));                                       \
+            goto u##k;                                                                  \
+        }                                                                               \
+        break;
                 GGS_FIRST(0) GGS_FIRST(1) GGS_FIRST(2) GGS_FIRST(3) GGS_FIRST(4)
                 GGS_FIRST(5) GGS_FIRST(6) GGS_FIRST(7)
 #undef GGS_FIRST
                 default: __builtin_unreachable();
             }
-#define GGS_MID(kp, k) u##kp: if (kB == k) goto last; if (k < NPK) GGS_PK(k, false);
+            // recurrence walk: f *= r, r *= rho (no exp)
+#define GGS_MID(kp, k)                                                                  \
+    u##kp:                                                                              \
+        if (kB == k) goto last;                                                         \
+        if (k < NPK) {                                                                  \
+            F2 = F2 * R2;                                                               \
+            R2 = R2 * (f2_t)s.rho;                                                      \
+            GGS_BLEND(k, F2);                                                           \
+        }
             GGS_MID(0, 1) GGS_MID(1, 2) GGS_MID(2, 3) GGS_MID(3, 4) GGS_MID(4, 5)
             GGS_MID(5, 6) GGS_MID(6, 7)
 #undef GGS_MID
         u7:
         last:
+            switch (kB) {
+#define GGS_LAST(k)                                                                     \
+    case k:                                                                             \
+        if (k < NPK) {                                                                  \
+            f2_t fu_ = F2 * R2;                                                         \
+            if ((unsigned)(8 * (k) - rlo) > rspan) fu_.x = 0.0f;                        \
+            if ((unsigned)(8 * (k) + 4 - rlo) > rspan) fu_.y = 0.0f;                    \
+            GGS_BLEND(k, fu_);                                                          \
+        }                                                                               \
+        break;
+                GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
+                GGS_LAST(7)
+#undef GGS_LAST
+                default: __builtin_unreachable();
+            }
+            goto done;
+            // exact walk (guard tripped): the exponent per pair as before
+#define GGS_XMID(kp, k) x##kp: if (kB == k) goto xlast; if (k < NPK) GGS_PK(k, false);
+            GGS_XMID(0, 1) GGS_XMID(1, 2) GGS_XMID(2, 3) GGS_XMID(3, 4) GGS_XMID(4, 5)
+            GGS_XMID(5, 6) GGS_XMID(6, 7)
+#undef GGS_XMID
+        x7:
+        xlast:
             switch (kB) {
 #define GGS_LAST(k) case k: if (k < NPK) GGS_PK(k, true); break;
                 GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
@@ -355,8 +428,8 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             GGS_MID(0, 1) GGS_MID(1, 2) GGS_MID(2, 3) GGS_MID(3, 4) GGS_MID(4, 5)
             GGS_MID(5, 6) GGS_MID(6, 7) GGS_MID(7, 8) GGS_MID(8, 9) GGS_MID(9, 10)
             GGS_MID(10, 11) GGS_MID(11, 12) GGS_MID(12, 13) GGS_MID(13, 14)
-#undef GGS_MID
             GGS_MID(14, 15)
+#undef GGS_MID
         u15:
         last:
             switch (gB) {
@@ -406,27 +479,28 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             }
         }
     } else {
+        // Branch-free: out-of-image pixels read a clamped address and count 0,
+        // so the loads of all rows can be in flight together.
         float acc = 0.0f, wacc = 0.0f;
-        if (col < W) {
+        const int ccol = min(col, W - 1);
 #pragma unroll
-            for (int g = 0; g < RG; ++g) {
-                const int row = ty0 + 4 * g + ph;
-                if (row < H) {
-                    const int64_t p = (int64_t)row * W + col;
-                    const float cr = fminf(fmaxf(__builtin_fmaf(T[g], bg_r, R[g]), 0.0f), 1.0f);
-                    const float cg = fminf(fmaxf(__builtin_fmaf(T[g], bg_g, G[g]), 0.0f), 1.0f);
-                    const float cb = fminf(fmaxf(__builtin_fmaf(T[g], bg_b, Bl[g]), 0.0f), 1.0f);
-                    const float dr = cr - target[p * 3 + 0];
-                    const float dg = cg - target[p * 3 + 1];
-                    const float db = cb - target[p * 3 + 2];
-                    const float d2 = dr * dr + dg * dg + db * db;
-                    float wgt = 1.0f;
-                    if (MODE == 2) wgt = mask[p];
-                    if (MODE == 3) wgt = 1.0f + beta * fminf(fmaxf(mask[p], 0.0f), 1.0f);
-                    acc += wgt * d2;
-                    wacc += wgt;
-                }
-            }
+        for (int g = 0; g < RG; ++g) {
+            const int row = ty0 + 4 * g + ph;
+            const bool ok = (row < H) & (col < W);
+            const int p = min(row, H - 1) * W + ccol;
+            const float cr = fminf(fmaxf(__builtin_fmaf(T[g], bg_r, R[g]), 0.0f), 1.0f);
+            const float cg = fminf(fmaxf(__builtin_fmaf(T[g], bg_g, G[g]), 0.0f), 1.0f);
+            const float cb = fminf(fmaxf(__builtin_fmaf(T[g], bg_b, Bl[g]), 0.0f), 1.0f);
+            const float dr = cr - target[(int64_t)p * 3 + 0];
+            const float dg = cg - target[(int64_t)p * 3 + 1];
+            const float db = cb - target[(int64_t)p * 3 + 2];
+            const float d2 = dr * dr + dg * dg + db * db;
+            float wgt = 1.0f;
+            if (MODE == 2) wgt = mask[p];
+            if (MODE == 3) wgt = 1.0f + beta * fminf(fmaxf(mask[p], 0.0f), 1.0f);
+            wgt = ok ? wgt : 0.0f;
+            acc += wgt * d2;
+            wacc += wgt;
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
