@@ -157,8 +157,8 @@ prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, f
 // raster
 // ---------------------------------------------------------------------------
 #ifndef GGS_ROWS
-#define GGS_ROWS 64
-#endif
+#define GGS_ROWS 128              // strip height: 32 pixels per lane (tools/ablate.py: 64 rows
+#endif                            // at 5 waves/SIMD 0.260 ms, 96 at 4: 0.249, 128 at 3: 0.249)
 constexpr int TILE = 64;          // tile width (pixels): 4 strips of 16 columns
 constexpr int TILE_H = GGS_ROWS;  // tile height (rows); one wave covers a 16 x TILE_H strip
 constexpr int RG = TILE_H / 4;    // row groups per lane (rows r, r+4, ...)
@@ -170,6 +170,9 @@ constexpr int WPB = GGS_WPB;      // waves per workgroup (each wave owns one 16-
 constexpr int NT = 64 * WPB;      // threads per workgroup
 constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
+#ifndef GGS_OCC
+#define GGS_OCC 3                 // waves per SIMD the register budget is sized for (158 VGPRs)
+#endif
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -181,7 +184,7 @@ __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirst
 // MASKED adds the per-lane row test for the AABB's first/last row block.
 // Performance-ablation switch (tools/ablate.py; 0 in every shipped build):
 // 1 = exp replaced by a multiply, 2 = no row-group bodies, 3 = red channel only,
-// 4 = cull + epilogue only (no per-splat work).
+// 4 = cull + epilogue only (no per-splat work), 5 = no epilogue, 6 = dispatch only.
 #ifndef GGS_ABL
 #define GGS_ABL 0
 #endif
@@ -209,6 +212,7 @@ __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirst
 #ifndef GGS_PACKED
 #define GGS_PACKED 1
 #endif
+static_assert(NPK <= 16 && (GGS_PACKED || RG <= 16), "walk macros cover 16 pairs / 16 groups");
 typedef float f2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_elementwise_fma(a, b, c); }
 #define GGS_PK(k, MASKED)                                                            \
@@ -240,6 +244,7 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
         P_T##k = P_T##k - w_;                                                        \
     } while (0)
 #define GGS_FOR8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+#define GGS_FOR16P(X) GGS_FOR8(X) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
 // MODE: 0 = write image, 1 = fitness/none, 2 = fitness/weighted, 3 = fitness/boost
 //
@@ -250,13 +255,17 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 // blends that list front-to-back, and writes its own partial sum.
 // 96 VGPRs -> 5 waves per SIMD (64 of them are the per-lane pixel accumulators).
 template <int MODE>
-__global__ void __launch_bounds__(NT, 5)
+__global__ void __launch_bounds__(NT, GGS_OCC)
 raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float* __restrict__ target, const float* __restrict__ mask, float beta,
               float* __restrict__ partials, float* __restrict__ wpartials,
               const int* __restrict__ tile_order) {
     __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
+    if (GGS_ABL == 6) {               // ablation: dispatch only
+        if (threadIdx.x == 0 && partials) partials[blockIdx.x] = 0.0f;
+        return;
+    }
 
     const int lane = threadIdx.x & 63;
     const int wib = ufirst((int)(threadIdx.x >> 6));  // wave in block (uniform: keeps control on SALU)
@@ -278,7 +287,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     // get vectorised into <16 x float> values whose phis the allocator splits.
 #if GGS_PACKED
 #define GGS_DECL(k) f2_t P_R##k = 0.0f, P_G##k = 0.0f, P_B##k = 0.0f, P_T##k = 1.0f;
-    GGS_FOR8(GGS_DECL)
+    GGS_FOR16P(GGS_DECL)
 #else
 #define GGS_DECL(g) float R##g = 0.0f, G##g = 0.0f, Bl##g = 0.0f, T##g = 1.0f;
     GGS_FOR16(GGS_DECL)
@@ -362,7 +371,9 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         }                                                                               \
         break;
                 GGS_FIRST(0) GGS_FIRST(1) GGS_FIRST(2) GGS_FIRST(3) GGS_FIRST(4)
-                GGS_FIRST(5) GGS_FIRST(6) GGS_FIRST(7)
+                GGS_FIRST(5) GGS_FIRST(6) GGS_FIRST(7) GGS_FIRST(8) GGS_FIRST(9)
+                GGS_FIRST(10) GGS_FIRST(11) GGS_FIRST(12) GGS_FIRST(13) GGS_FIRST(14)
+                GGS_FIRST(15)
 #undef GGS_FIRST
                 default: __builtin_unreachable();
             }
@@ -376,9 +387,10 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             GGS_BLEND(k, F2);                                                           \
         }
             GGS_MID(0, 1) GGS_MID(1, 2) GGS_MID(2, 3) GGS_MID(3, 4) GGS_MID(4, 5)
-            GGS_MID(5, 6) GGS_MID(6, 7)
+            GGS_MID(5, 6) GGS_MID(6, 7) GGS_MID(7, 8) GGS_MID(8, 9) GGS_MID(9, 10)
+            GGS_MID(10, 11) GGS_MID(11, 12) GGS_MID(12, 13) GGS_MID(13, 14) GGS_MID(14, 15)
 #undef GGS_MID
-        u7:
+        u15:
         last:
             switch (kB) {
 #define GGS_LAST(k)                                                                     \
@@ -391,7 +403,8 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         }                                                                               \
         break;
                 GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
-                GGS_LAST(7)
+                GGS_LAST(7) GGS_LAST(8) GGS_LAST(9) GGS_LAST(10) GGS_LAST(11) GGS_LAST(12)
+                GGS_LAST(13) GGS_LAST(14) GGS_LAST(15)
 #undef GGS_LAST
                 default: __builtin_unreachable();
             }
@@ -399,14 +412,17 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             // exact walk (guard tripped): the exponent per pair as before
 #define GGS_XMID(kp, k) x##kp: if (kB == k) goto xlast; if (k < NPK) GGS_PK(k, false);
             GGS_XMID(0, 1) GGS_XMID(1, 2) GGS_XMID(2, 3) GGS_XMID(3, 4) GGS_XMID(4, 5)
-            GGS_XMID(5, 6) GGS_XMID(6, 7)
+            GGS_XMID(5, 6) GGS_XMID(6, 7) GGS_XMID(7, 8) GGS_XMID(8, 9) GGS_XMID(9, 10)
+            GGS_XMID(10, 11) GGS_XMID(11, 12) GGS_XMID(12, 13) GGS_XMID(13, 14)
+            GGS_XMID(14, 15)
 #undef GGS_XMID
-        x7:
+        x15:
         xlast:
             switch (kB) {
 #define GGS_LAST(k) case k: if (k < NPK) GGS_PK(k, true); break;
                 GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
-                GGS_LAST(7)
+                GGS_LAST(7) GGS_LAST(8) GGS_LAST(9) GGS_LAST(10) GGS_LAST(11) GGS_LAST(12)
+                GGS_LAST(13) GGS_LAST(14) GGS_LAST(15)
 #undef GGS_LAST
                 default: __builtin_unreachable();
             }
@@ -451,6 +467,10 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     }
 
     // --- epilogue ---------------------------------------------------------------
+    if (GGS_ABL == 5) {               // ablation: no epilogue
+        if (lane == 0 && MODE != 0) partials[((int64_t)b * nTiles + t) * 4 + wv] = (float)cnt;
+        return;
+    }
     float R[RG], G[RG], Bl[RG], T[RG];
 #if GGS_PACKED
 #define GGS_PACK(k)                                                                   \
@@ -459,7 +479,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         R[2 * k + 1] = P_R##k.y; G[2 * k + 1] = P_G##k.y; Bl[2 * k + 1] = P_B##k.y;   \
         T[2 * k + 1] = P_T##k.y;                                                      \
     }
-    GGS_FOR8(GGS_PACK)
+    GGS_FOR16P(GGS_PACK)
 #else
 #define GGS_PACK(g) if (g < RG) { R[g] = R##g; G[g] = G##g; Bl[g] = Bl##g; T[g] = T##g; }
     GGS_FOR16(GGS_PACK)
