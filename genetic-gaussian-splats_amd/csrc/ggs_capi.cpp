@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -86,8 +87,9 @@ int ensure_pinned(PinBuf& b, size_t bytes) {
 // Per-(device, stream) scratch used by one render/fitness pipeline.
 struct Workspace {
     hipStream_t stream = nullptr;
-    DevBuf recs, partials, wpartials, order;
+    DevBuf recs, partials, wpartials, order, plan;
     int order_H = -1, order_W = -1;   // (H, W) the tile order was built for
+    uint64_t plan_key = 0;            // inputs the plan was built from (0: none / volatile)
 };
 
 // Upload the central-tiles-first raster order for (H, W) once per size.
@@ -286,9 +288,16 @@ int check_dims(int64_t B, int32_t N, int32_t C, int32_t H, int32_t W) {
 }
 
 // ---- the device pipelines (ctx locked, device set) ----------------------------------
+int run_fitness_planned(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, int C,
+                        const float4* plan, const float* wpartials, int mode, int H, int W, float k,
+                        float* d_out);
+
+// plan_key: identifies (target contents, mask contents, mode, beta, H, W) when
+// the caller knows them to be unchanged since a previous call with the same key
+// (host API: content hashes; GA/SA sessions: immutable inputs); 0 = rebuild.
 int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, int C,
                 const float* d_target, const float* d_mask, int mode, float beta, int H, int W,
-                float k, float* d_out) {
+                float k, float* d_out, uint64_t plan_key = 0) {
     if (B == 0) return GGS_OK;
     Workspace* w = workspace_for(c, st);
     int nTX;
@@ -299,6 +308,28 @@ int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N,
     if ((rc = ensure(w->partials, sizeof(float) * 4 * (size_t)(B * nTiles), st))) return rc;
     if ((rc = ensure(w->wpartials, sizeof(float) * 4 * (size_t)nTiles, st))) return rc;
     if ((rc = ensure_tile_order(w, H, W, st))) return rc;
+    if (plan_key == 0 || plan_key != w->plan_key) {
+        if ((rc = ensure(w->plan, plan_bytes(H, W), st))) return rc;
+        GGS_HIP(launch_plan(st, d_target, d_mask, mode, beta, H, W, (float4*)w->plan.p,
+                            (float*)w->wpartials.p));
+        w->plan_key = plan_key;
+    }
+    return run_fitness_planned(c, st, d_gen, B, N, C, (const float4*)w->plan.p,
+                               (const float*)w->wpartials.p, mode, H, W, k, d_out);
+}
+
+// prep -> raster -> finalize against a ready target plan.
+int run_fitness_planned(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, int C,
+                        const float4* plan, const float* wpartials, int mode, int H, int W, float k,
+                        float* d_out) {
+    if (B == 0) return GGS_OK;
+    Workspace* w = workspace_for(c, st);
+    int nTX;
+    const int nTiles = raster_tiles(H, W, &nTX);
+    int rc;
+    if ((rc = ensure(w->recs, sizeof(SplatRec) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
+    if ((rc = ensure(w->partials, sizeof(float) * 4 * (size_t)(B * nTiles), st))) return rc;
+    if ((rc = ensure_tile_order(w, H, W, st))) return rc;
     SplatRec* recs = (SplatRec*)w->recs.p;
     {
         ProfScope ps(st, 0);
@@ -307,13 +338,13 @@ int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N,
     const float bg[3] = {1.f, 1.f, 1.f};  // fitness renders with the default background (fitness.py:15)
     {
         ProfScope ps(st, 1);
-        GGS_HIP(launch_raster(st, 1 + mode, recs, (int)B, N, H, W, bg, nullptr, d_target, d_mask, beta,
-                              (float*)w->partials.p, (float*)w->wpartials.p, (const int*)w->order.p));
+        GGS_HIP(launch_raster(st, 1, recs, (int)B, N, H, W, bg, nullptr, plan, (float*)w->partials.p,
+                              (const int*)w->order.p));
     }
     {
         ProfScope ps(st, 2);
-        GGS_HIP(launch_finalize(st, (const float*)w->partials.p, (const float*)w->wpartials.p, (int)B,
-                                nTiles, mode, H, W, d_out));
+        GGS_HIP(launch_finalize(st, (const float*)w->partials.p, wpartials, (int)B, nTiles, mode, H, W,
+                                d_out));
     }
     return GGS_OK;
 }
@@ -332,8 +363,8 @@ int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, 
     }
     {
         ProfScope ps(st, 1);
-        GGS_HIP(launch_raster(st, 0, recs, (int)B, N, H, W, bg, d_img, nullptr, nullptr, 0.f, nullptr,
-                              nullptr, (const int*)w->order.p));
+        GGS_HIP(launch_raster(st, 0, recs, (int)B, N, H, W, bg, d_img, nullptr, nullptr,
+                              (const int*)w->order.p));
     }
     return GGS_OK;
 }
@@ -429,6 +460,80 @@ int ggs_fitness_device(int32_t device, void* stream, const float* d_genomes_axes
                        boost_beta, H, W, k_sigma, d_out_B);
 }
 
+// ---- target plans (device API with a target prepared once) ------------------
+}  // extern "C"
+namespace ggs {
+namespace {
+struct TargetPlan {
+    DevCtx* c = nullptr;
+    int H = 0, W = 0, mode = 0;
+    DevBuf plan, wpartials;
+};
+}  // namespace
+}  // namespace ggs
+extern "C" {
+
+int ggs_plan_create(int32_t device, void* stream, const float* d_target_hw3, const float* d_mask_hw,
+                    int32_t mode, float boost_beta, int32_t H, int32_t W, void** plan) {
+    int rc = check_dims(1, 1, 9, H, W);
+    if (rc) return rc;
+    if (!plan || !d_target_hw3) return fail(GGS_EINVAL, "null argument");
+    if (mode < GGS_FIT_NONE || mode > GGS_FIT_BOOST) return fail(GGS_EINVAL, "bad fitness mode %d", mode);
+    if (mode != GGS_FIT_NONE && !d_mask_hw) return fail(GGS_EINVAL, "mode %d needs a weight mask", mode);
+    DevCtx* c = nullptr;
+    if ((rc = get_ctx(device, &c))) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->dev);
+    auto p = std::make_unique<TargetPlan>();
+    p->c = c;
+    p->H = H;
+    p->W = W;
+    p->mode = mode;
+    const hipStream_t st = (hipStream_t)stream;
+    int nTX;
+    const int nTiles = raster_tiles(H, W, &nTX);
+    auto bail = [&](int code) {
+        if (p->plan.p) (void)hipFree(p->plan.p);
+        if (p->wpartials.p) (void)hipFree(p->wpartials.p);
+        return code;
+    };
+    if ((rc = ensure(p->plan, plan_bytes(H, W), st)) ||
+        (rc = ensure(p->wpartials, sizeof(float) * 4 * (size_t)nTiles, st)))
+        return bail(rc);
+    if (launch_plan(st, d_target_hw3, d_mask_hw, mode, boost_beta, H, W, (float4*)p->plan.p,
+                    (float*)p->wpartials.p) != hipSuccess)
+        return bail(fail(GGS_EHIP, "plan launch failed"));
+    *plan = p.release();
+    return GGS_OK;
+}
+
+int ggs_fitness_device_planned(void* plan, void* stream, const float* d_genomes_axes, int64_t B,
+                               int32_t N, int32_t C, float k_sigma, float* d_out_B) {
+    if (!plan) return fail(GGS_EINVAL, "null plan");
+    TargetPlan* p = (TargetPlan*)plan;
+    int rc = check_dims(B, N, C, p->H, p->W);
+    if (rc) return rc;
+    if (B > 0 && ((!d_genomes_axes && N > 0) || !d_out_B)) return fail(GGS_EINVAL, "null pointer");
+    std::lock_guard<std::mutex> lk(p->c->mu);
+    DeviceGuard dg(p->c->dev);
+    return run_fitness_planned(p->c, (hipStream_t)stream, d_genomes_axes, B, N, C,
+                               (const float4*)p->plan.p, (const float*)p->wpartials.p, p->mode, p->H,
+                               p->W, k_sigma, d_out_B);
+}
+
+void ggs_plan_destroy(void* plan) {
+    if (!plan) return;
+    TargetPlan* p = (TargetPlan*)plan;
+    {
+        std::lock_guard<std::mutex> lk(p->c->mu);
+        DeviceGuard dg(p->c->dev);
+        (void)hipDeviceSynchronize();    // streams that may still read the plan
+        if (p->plan.p) (void)hipFree(p->plan.p);
+        if (p->wpartials.p) (void)hipFree(p->wpartials.p);
+    }
+    delete p;
+}
+
 int ggs_render_device(int32_t device, void* stream, const float* d_genomes, int64_t B, int32_t N,
                       int32_t C, int32_t H, int32_t W, float k_sigma, const float* bg,
                       float* d_out_bhw3) {
@@ -494,9 +599,14 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
             memcpy(c->h_gen.p, genomes_axes + row * b0, gbytes);
             GGS_HIP(hipMemcpyAsync(c->gen.p, c->h_gen.p, gbytes, hipMemcpyHostToDevice, st));
         }
+        uint32_t bb;
+        memcpy(&bb, &boost_beta, 4);
+        const uint64_t pkey = ((tkey * 0x9E3779B97F4A7C15ull) ^ (mkey + 0x632BE59BD9B4E019ull) ^
+                               ((uint64_t)bb << 8) ^ ((uint64_t)mode << 2) ^ ((uint64_t)H << 40) ^
+                               ((uint64_t)W << 20)) & ~(1ull << 63);
         if ((rc = run_fitness(c, st, (const float*)c->gen.p, nb, N, C, (const float*)c->target.p,
                               mask_hw ? (const float*)c->mask.p : nullptr, mode, boost_beta, H, W,
-                              k_sigma, (float*)c->out.p)))
+                              k_sigma, (float*)c->out.p, pkey | 1)))
             return rc;
         GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, sizeof(float) * nb, hipMemcpyDeviceToHost, st));
     }
@@ -669,7 +779,13 @@ void ggs_profile_reset(void) {
 namespace ggs {
 namespace {
 
+// Target-plan cache keys of sessions (their target/mask never change): unique
+// for the process lifetime, top bit set (host-API content keys have it clear).
+std::atomic<uint64_t> g_session_ids{0};
+uint64_t new_plan_id() { return (1ull << 63) | ++g_session_ids; }
+
 struct GaSession {
+    uint64_t plan_id = new_plan_id();
     DevCtx* c = nullptr;
     hipStream_t st = nullptr;
     ggs_ga_config cfg{};
@@ -771,7 +887,8 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
                                 P, N, prm, d, s->cfg.seed, gen, (float*)s->off.p, P));
     if ((rc = run_fitness(s->c, s->st, (const float*)s->off.p, P, N, 9, (const float*)s->target.p,
                           s->mask.p ? (const float*)s->mask.p : nullptr, s->cfg.fitness_mode,
-                          s->cfg.boost_beta, s->cfg.H, s->cfg.W, s->cfg.k_sigma, (float*)s->off_fits.p)))
+                          s->cfg.boost_beta, s->cfg.H, s->cfg.W, s->cfg.k_sigma, (float*)s->off_fits.p,
+                          s->plan_id)))
         return rc;
     double* row;
     if ((rc = ga_curves_row(s, &row))) return rc;
@@ -785,6 +902,7 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
 }
 
 struct SaSession {
+    uint64_t plan_id = new_plan_id();
     DevCtx* c = nullptr;
     hipStream_t st = nullptr;
     ggs_ga_config cfg{};
@@ -803,7 +921,7 @@ void sa_free(SaSession* s) {
 int sa_eval(SaSession* s, const float* G, int n, float* dev_out) {
     return run_fitness(s->c, s->st, G, n, s->N, 9, (const float*)s->target.p,
                        s->mask.p ? (const float*)s->mask.p : nullptr, s->cfg.fitness_mode,
-                       s->cfg.boost_beta, s->cfg.H, s->cfg.W, s->cfg.k_sigma, dev_out);
+                       s->cfg.boost_beta, s->cfg.H, s->cfg.W, s->cfg.k_sigma, dev_out, s->plan_id);
 }
 
 // Shared validation of ggs_ga_create / ggs_sa_create.
@@ -877,7 +995,7 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
         return bail(fail(GGS_EHIP, "upload failed"));
     if ((rc = run_fitness(ctx, s->st, (const float*)s->pop[0].p, s->P, s->N, 9, (const float*)s->target.p,
                           mask_hw ? (const float*)s->mask.p : nullptr, c.fitness_mode, c.boost_beta,
-                          c.H, c.W, c.k_sigma, (float*)s->fits[0].p)))
+                          c.H, c.W, c.k_sigma, (float*)s->fits[0].p, s->plan_id)))
         return bail(rc);
     double* row;
     if ((rc = ga_curves_row(s.get(), &row))) return bail(rc);

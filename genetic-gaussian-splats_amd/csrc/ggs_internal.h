@@ -25,8 +25,12 @@ hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_
                        int W, float k, SplatRec* recs, float* f9, int* i4, float* enc9);
 int raster_tiles(int H, int W, int* nTX);
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
-                         const float bg[3], float* img, const float* target, const float* mask,
-                         float beta, float* partials, float* wpartials, const int* tile_order);
+                         const float bg[3], float* img, const float4* plan, float* partials,
+                         const int* tile_order);
+// Target plan for the fitness epilogue (built once per target/mask/mode/beta).
+hipError_t launch_plan(hipStream_t st, const float* target, const float* mask, int mode, float beta,
+                       int H, int W, float4* plan, float* wpartials);
+size_t plan_bytes(int H, int W);
 // Tile visiting order for the raster grid: tiles sorted by distance of their
 // centre from the image centre (central tiles carry the most splats; running
 // them first shortens the tail of the launch).

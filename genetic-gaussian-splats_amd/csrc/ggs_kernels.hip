@@ -252,7 +252,7 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 #define GGS_FOR8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #define GGS_FOR16P(X) GGS_FOR8(X) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
-// MODE: 0 = write image, 1 = fitness/none, 2 = fitness/weighted, 3 = fitness/boost
+// MODE: 0 = write image, 1 = fitness (weights from the target plan)
 //
 // Workgroup = 4 independent wave64s on one 64x64 tile; wave w owns the 16-column
 // strip [tx0+16w, tx0+16w+15] x 64 rows.  No workgroup barrier anywhere: each
@@ -264,8 +264,7 @@ template <int MODE>
 __global__ void __launch_bounds__(NT, GGS_OCC)
 raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
-              const float* __restrict__ target, const float* __restrict__ mask, float beta,
-              float* __restrict__ partials, float* __restrict__ wpartials,
+              const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order) {
     __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
     if (GGS_ABL == 6) {               // ablation: dispatch only
@@ -510,41 +509,75 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             }
         }
     } else {
-        // Branch-free: out-of-image pixels read a clamped address and count 0,
-        // so the loads of all rows can be in flight together.
-        float acc = 0.0f, wacc = 0.0f;
-        const int ccol = min(col, W - 1);
+        // The target plan (plan_kernel) holds (t_r, t_g, t_b, w) per pixel in this
+        // wave's lane order, w already mode-specific and 0 outside the image:
+        // one coalesced 16-B load per pixel, no address math, no bounds tests.
+        float acc = 0.0f;
+        const float4* __restrict__ P = plan + (int64_t)(t * 4 + wv) * RG * 64 + lane;
 #pragma unroll
         for (int g = 0; g < RG; ++g) {
-            const int row = ty0 + 4 * g + ph;
-            const bool ok = (row < H) & (col < W);
-            const int p = min(row, H - 1) * W + ccol;
+            const float4 q = P[g * 64];
             const float cr = fminf(fmaxf(__builtin_fmaf(T[g], bg_r, R[g]), 0.0f), 1.0f);
             const float cg = fminf(fmaxf(__builtin_fmaf(T[g], bg_g, G[g]), 0.0f), 1.0f);
             const float cb = fminf(fmaxf(__builtin_fmaf(T[g], bg_b, Bl[g]), 0.0f), 1.0f);
-            const float dr = cr - target[(int64_t)p * 3 + 0];
-            const float dg = cg - target[(int64_t)p * 3 + 1];
-            const float db = cb - target[(int64_t)p * 3 + 2];
+            const float dr = cr - q.x;
+            const float dg = cg - q.y;
+            const float db = cb - q.z;
             const float d2 = dr * dr + dg * dg + db * db;
-            float wgt = 1.0f;
-            if (MODE == 2) wgt = mask[p];
-            if (MODE == 3) wgt = 1.0f + beta * fminf(fmaxf(mask[p], 0.0f), 1.0f);
-            wgt = ok ? wgt : 0.0f;
-            acc += wgt * d2;
-            wacc += wgt;
+            acc += q.w * d2;
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            acc += __shfl_xor(acc, o);
-            wacc += __shfl_xor(wacc, o);
-        }
-        if (lane == 0) {      // one partial per (candidate, tile, strip): no block barrier
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0)        // one partial per (candidate, tile, strip): no block barrier
             partials[((int64_t)b * nTiles + t) * 4 + wv] = acc;
-            if (b == 0 && wpartials) wpartials[t * 4 + wv] = wacc;
-        }
     }
 }
 #undef GGS_PAIR
+
+// ---------------------------------------------------------------------------
+// target plan: the fitness epilogue's inputs re-laid out in raster lane order
+// ---------------------------------------------------------------------------
+// One wave per (tile, strip): plan[((t*4 + strip)*RG + g)*64 + lane] =
+// (t_r, t_g, t_b, w) of the pixel that lane owns in row group g; w is the
+// pixel weight of fitness.py:17-31 for the mode (1 / mask / 1+beta*clamp(mask))
+// and 0 outside the image.  wpartials[t*4 + strip] = the strip's sum of w
+// (per-lane in row order, then a lane butterfly).  Target and mask are constant
+// over a GA run, so the plan is built once per (target, mask, mode, beta).
+__global__ void __launch_bounds__(64)
+plan_kernel(const float* __restrict__ target, const float* __restrict__ mask, int mode, float beta,
+            int H, int W, int nTX, float4* __restrict__ plan, float* __restrict__ wpartials) {
+    const int lane = threadIdx.x;
+    const int t = blockIdx.x >> 2, wv = blockIdx.x & 3;
+    const int tx0 = (t % nTX) * TILE, ty0 = (t / nTX) * TILE_H;
+    const int col = tx0 + wv * 16 + (lane & 15), ph = lane >> 4;
+    float4* __restrict__ P = plan + (int64_t)blockIdx.x * RG * 64 + lane;
+    float wacc = 0.0f;
+    for (int g = 0; g < RG; ++g) {
+        const int row = ty0 + 4 * g + ph;
+        const bool ok = (row < H) & (col < W);
+        const int64_t p = (int64_t)min(row, H - 1) * W + min(col, W - 1);
+        float wgt = 1.0f;
+        if (mode == GGS_FIT_WEIGHTED) wgt = mask[p];
+        if (mode == GGS_FIT_BOOST) wgt = 1.0f + beta * fminf(fmaxf(mask[p], 0.0f), 1.0f);
+        wgt = ok ? wgt : 0.0f;
+        P[g * 64] = make_float4(target[p * 3 + 0], target[p * 3 + 1], target[p * 3 + 2], wgt);
+        wacc += wgt;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wacc += __shfl_xor(wacc, o);
+    if (lane == 0) wpartials[blockIdx.x] = wacc;
+}
+
+hipError_t launch_plan(hipStream_t st, const float* target, const float* mask, int mode, float beta,
+                       int H, int W, float4* plan, float* wpartials) {
+    int nTX;
+    const int nTiles = raster_tiles(H, W, &nTX);
+    hipLaunchKernelGGL(plan_kernel, dim3(nTiles * 4), dim3(64), 0, st, target, mask, mode, beta, H, W, nTX,
+                       plan, wpartials);
+    return hipGetLastError();
+}
+
+size_t plan_bytes(int H, int W) { return sizeof(float4) * 4 * (size_t)raster_tiles(H, W, nullptr) * RG * 64; }
 
 // ---------------------------------------------------------------------------
 // finalize: fixed-order float64 reduction of tile partials -> fitness scalar
@@ -643,20 +676,16 @@ int raster_tiles(int H, int W, int* nTX) {
 }
 
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
-                         const float bg[3], float* img, const float* target, const float* mask,
-                         float beta, float* partials, float* wpartials, const int* tile_order) {
+                         const float bg[3], float* img, const float4* plan, float* partials,
+                         const int* tile_order) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
 #define GGS_RASTER(M)                                                                          \
     hipLaunchKernelGGL(raster_kernel<M>, grid, block, 0, st, recs, B, N, H, W, nTX, nTiles,     \
-                       bg[0], bg[1], bg[2], img, target, mask, beta, partials, wpartials, tile_order)
-    switch (mode) {
-        case 0: GGS_RASTER(0); break;
-        case 1: GGS_RASTER(1); break;
-        case 2: GGS_RASTER(2); break;
-        default: GGS_RASTER(3); break;
-    }
+                       bg[0], bg[1], bg[2], img, plan, partials, tile_order)
+    if (mode == 0) GGS_RASTER(0);      // image
+    else GGS_RASTER(1);                // fitness: the mode lives in the plan's weights
 #undef GGS_RASTER
     return hipGetLastError();
 }

@@ -64,6 +64,11 @@ SIGNATURES = {
     "ggs_profile_enable": (C.c_int, [C.c_int32]),
     "ggs_profile_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "ggs_profile_reset": (None, []),
+    "ggs_plan_create": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                  C.c_float, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "ggs_fitness_device_planned": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                             C.c_int32, C.c_int32, C.c_float, C.c_void_p]),
+    "ggs_plan_destroy": (None, [C.c_void_p]),
     "ggs_ga_create": (C.c_int, [C.c_int32, C.POINTER(GaConfig), _f32p, _f32p, _f32p,
                                 C.POINTER(C.c_void_p)]),
     "ggs_ga_step": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(GaDraws)]),

@@ -141,6 +141,37 @@ def fitness_device(device: int, stream: int, d_genomes: int, B: int, N: int, Cc:
           "ggs_fitness_device")
 
 
+class TargetPlan:
+    """A target/mask prepared once for ``ggs_fitness_device_planned`` (the GA's
+    fixed target over a run).  Pointers are device pointers on ``device``; the
+    plan is built on ``stream``."""
+
+    def __init__(self, device: int, stream: int, d_target: int, d_mask: int, mode: int,
+                 boost_beta: float, H: int, W: int):
+        h = C.c_void_p()
+        check(lib.ggs_plan_create(device, C.c_void_p(stream), C.c_void_p(d_target),
+                                  C.c_void_p(d_mask or None), mode, float(boost_beta), H, W,
+                                  C.byref(h)), "ggs_plan_create")
+        self.h, self.H, self.W = h, H, W
+
+    def fitness_device(self, stream: int, d_genomes: int, B: int, N: int, Cc: int,
+                       k_sigma: float, d_out: int) -> None:
+        check(lib.ggs_fitness_device_planned(self.h, C.c_void_p(stream), C.c_void_p(d_genomes), B,
+                                             N, Cc, float(k_sigma), C.c_void_p(d_out)),
+              "ggs_fitness_device_planned")
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib.ggs_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 — interpreter shutdown
+            pass
+
+
 def render_device(device: int, stream: int, d_genomes: int, B: int, N: int, Cc: int, H: int,
                   W: int, k_sigma: float, d_out: int, background=(1.0, 1.0, 1.0)) -> None:
     bg = np.ascontiguousarray(np.broadcast_to(np.asarray(background, np.float32), (3,)))

@@ -115,6 +115,17 @@ int ggs_fitness_device(int32_t device, void* stream, const float* d_genomes_axes
                        int32_t mode, float boost_beta, int32_t H, int32_t W, float k_sigma,
                        float* d_out_B);
 
+/* Target plan: the fitness epilogue's inputs (target, mask, mode, beta) laid out
+ * once in the raster's lane order — what ggs_fitness_device rebuilds on every
+ * call.  A caller whose target/mask stay fixed over a run (a GA loop) builds it
+ * once (enqueued on `stream`; the inputs must stay valid until it has run) and
+ * evaluates generations with ggs_fitness_device_planned (same results). */
+int ggs_plan_create(int32_t device, void* stream, const float* d_target_hw3, const float* d_mask_hw,
+                    int32_t mode, float boost_beta, int32_t H, int32_t W, void** plan);
+int ggs_fitness_device_planned(void* plan, void* stream, const float* d_genomes_axes, int64_t B,
+                               int32_t N, int32_t C, float k_sigma, float* d_out_B);
+void ggs_plan_destroy(void* plan);
+
 /* ---- device-resident GA ------------------------------
  * genetic_approx's generation loop (algorithm.py:85-155) on one device: the
  * population, fitness, elites, best individual and curves stay in HBM; a

@@ -309,7 +309,16 @@ def test_device_api_matches_host_api(full_size):
         torch.cuda.synchronize()
         kw = {} if mode == ggs.GGS_FIT_NONE else {"weight_mask": mask,
                                                   "boost_only": mode == ggs.GGS_FIT_BOOST}
-        np.testing.assert_array_equal(out.cpu().numpy(), ggs.fitness(pop[:16], tgt, H, W, 3.0, **kw))
+        ref = ggs.fitness(pop[:16], tgt, H, W, 3.0, **kw)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+        # target plan built once, reused across calls: same bits
+        plan = ggs.TargetPlan(0, st, dt.data_ptr(), m, mode, 1.0, H, W)
+        for _ in range(2):
+            out.zero_()
+            plan.fitness_device(st, dg.data_ptr(), 16, 256, 9, 3.0, out.data_ptr())
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy(), ref)
+        plan.close()
     img = torch.empty((2, H, W, 3), dtype=torch.float32, device=dev)
     g9 = torch.from_numpy(ggs.encode(pop[:2])).to(dev)
     ggs.render_device(0, st, g9.data_ptr(), 2, 256, 9, H, W, 3.0, img.data_ptr())
