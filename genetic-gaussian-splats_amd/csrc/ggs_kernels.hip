@@ -287,6 +287,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     const int ph = lane >> 4;         // row phase 0..3
     const float Xf = (float)col;
     const float Yb = (float)(ty0 + ph);
+    const int rowb = ty0 + ph;        // this lane's row in row group 0
 
     // 16 pixels per lane x (R, G, B, transmittance), as named scalars: arrays
     // get vectorised into <16 x float> values whose phis the allocator splits.
@@ -351,7 +352,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             f2_t F2, R2;                                       // row recurrence: f, ratio
             // First pair: exact exponent; keeps the unmasked f as the recurrence
             // seed and, when more pairs follow, the ratio 2^d to the next pair.
-            // A seed below 2^-100 on a live lane (tiny corner of a thin rotated
+            // A seed below 2^-100 (0x0D800000) on a live lane (tiny corner of a thin rotated
             // splat) would lose the recurrence's precision: that wave walks this
             // splat with the exact exponent instead (wave-uniform, ~0.3 % of walks).
             switch (kA) {
@@ -363,11 +364,19 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             F2.x = GGS_EXP2(e_.x);                                                      \
             F2.y = GGS_EXP2(e_.y);                                                      \
             f2_t fu_ = F2;                                                              \
-            if ((unsigned)(8 * (k) - rlo) > rspan) fu_.x = 0.0f;                        \
-            if ((unsigned)(8 * (k) + 4 - rlo) > rspan) fu_.y = 0.0f;                    \
+            if (kB == k) {                /* one pair: both AABB row limits */          \
+                if ((unsigned)(8 * (k) - rlo) > rspan) fu_.x = 0.0f;                    \
+                if ((unsigned)(8 * (k) + 4 - rlo) > rspan) fu_.y = 0.0f;                \
+                GGS_BLEND(k, fu_);                                                      \
+                goto done;                                                              \
+            }                                                                           \
+            if (rowb < y0 - 8 * (k)) fu_.x = 0.0f;          /* rows above y0 */         \
+            if (rowb < y0 - 8 * (k) - 4) fu_.y = 0.0f;                                  \
             GGS_BLEND(k, fu_);                                                          \
-            if (kB == k) goto done;                                                     \
-            if (__ballot(inx && fminf(e_.x, e_.y) < -100.0f)) goto x##k;                \
+            /* guard on the seed's bits (f >= 0: unsigned order = float order)  */      \
+            if (__ballot(inx) & __ballot((__float_as_uint(F2.x) < 0x0D800000u) |       \
+                                         (__float_as_uint(F2.y) < 0x0D800000u)))        \
+                goto x##k;                                                              \
             const float t8_ = __builtin_fmaf(bx, 8.0f, s.c64);                          \
             f2_t d_ = fma2(qy_, (f2_t)s.c16, (f2_t)t8_);                                \
             R2.x = GGS_EXP2(fminf(d_.x, 100.0f));                                       \
@@ -407,8 +416,8 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     case k:                                                                             \
         if (k < NPK) {                                                                  \
             f2_t fu_ = F2 * R2;                                                         \
-            if ((unsigned)(8 * (k) - rlo) > rspan) fu_.x = 0.0f;                        \
-            if ((unsigned)(8 * (k) + 4 - rlo) > rspan) fu_.y = 0.0f;                    \
+            if (rowb > y1 - 8 * (k)) fu_.x = 0.0f;          /* rows below y1 */         \
+            if (rowb > y1 - 8 * (k) - 4) fu_.y = 0.0f;                                  \
             GGS_BLEND(k, fu_);                                                          \
         }                                                                               \
         break;
