@@ -7,22 +7,25 @@
 //   raster      _render_tile_over_kernel (Triton)  modules/render.py:121-200
 //   epilogue    canvas fill / clamp / L2 fitness   modules/render.py:235-252, fitness.py:16-31
 //
-// Three launches per batch (fitness) — prep, raster, finalize; two for render.
+// Three launches per batch (fitness) — prep, raster, finalize; two for render;
+// plus plan once per fitness target.
 //   prep     1 thread / splat: encode (fitness) + preprocess -> 64-B SplatRec in HBM.
 //            Bounds-critical math is ggs_detmath.h (bit-exact with oracle/).
-//   raster   1 workgroup (4 wave64) / (candidate, 64x64 tile).  Order-preserving
-//            cull of the candidate's N splats against the tile (wave ballot +
+//   raster   1 wave64 / (candidate, 64x128 tile, 16-column strip).  Order-preserving
+//            cull of the candidate's N splats against the strip (wave ballot +
 //            mbcnt compaction, no global sort) into an LDS list, then a front-to-
-//            back per-pixel blend: wave w owns a 16-column x 64-row strip; lane
-//            (c, r) owns column c and rows r, r+4, ..., r+60 (16 pixels held in
-//            registers).  Per splat the x-dependent half of the Gaussian exponent
-//            is formed once per lane; row groups outside the splat's AABB are
-//            skipped wave-uniformly (scalar branches on readfirstlane'd bounds).
-//            Epilogue: background + clamp, then either the image store (render)
-//            or the weighted squared error summed per tile (fitness; the image
-//            never touches HBM).
-//   finalize 1 workgroup / candidate: fixed-order float64 sum of the tile
+//            back per-pixel blend: lane (c, r) owns column c and rows r, r+4, ...,
+//            r+124 (32 pixels held in registers, two rows per packed op).  Per
+//            splat the x-dependent half of the Gaussian exponent is formed once
+//            per lane; the first row pair gets the exact exponent, further pairs
+//            a multiplicative row recurrence (no exp); row ranges outside the
+//            splat's AABB are skipped wave-uniformly.  Epilogue: background +
+//            clamp, then either the image store (render) or the weighted squared
+//            error against the target plan, summed per strip (the image never
+//            touches HBM).
+//   finalize 1 workgroup / candidate: fixed-order float64 sum of the strip
 //            partials -> the fitness scalar (deterministic, no atomics).
+//   plan     1 wave / (tile, strip): target + mode weights in raster lane order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -254,12 +257,12 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 
 // MODE: 0 = write image, 1 = fitness (weights from the target plan)
 //
-// Workgroup = 4 independent wave64s on one 64x64 tile; wave w owns the 16-column
-// strip [tx0+16w, tx0+16w+15] x 64 rows.  No workgroup barrier anywhere: each
-// wave culls the candidate's splats against its own strip (64 per step, highest
-// index first, ballot + mbcnt compaction -> an order-preserving LDS list),
-// blends that list front-to-back, and writes its own partial sum.
-// 96 VGPRs -> 5 waves per SIMD (64 of them are the per-lane pixel accumulators).
+// One wave per workgroup (GGS_WPB); wave w of a 64 x TILE_H tile owns the
+// 16-column strip [tx0+16w, tx0+16w+15] x TILE_H rows.  No workgroup barrier
+// anywhere: each wave culls the candidate's splats against its own strip (64
+// per step, highest index first, ballot + mbcnt compaction -> an order-
+// preserving LDS list), blends that list front-to-back, and writes its own
+// partial sum.  TILE_H = 128: 128 accumulator VGPRs (+~35) -> 3 waves per SIMD.
 template <int MODE>
 __global__ void __launch_bounds__(NT, GGS_OCC)
 raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
