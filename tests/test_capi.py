@@ -168,3 +168,33 @@ def test_drop_in_keeps_module_constant():
 def test_package_layout():
     assert os.path.isfile(os.path.join(PKG, "libggs.so"))
     assert os.path.isdir(os.path.join(PKG, "csrc"))
+
+
+def _build_c_host(tmp_path):
+    from ggs import _lib
+    exe = os.path.join(tmp_path, "ggs_c_host")
+    src = os.path.join(os.path.dirname(__file__), "c", "ggs_c_host.c")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"),
+                    src, "-o", exe, "-L", libdir, "-lggs", "-Wl,-rpath," + libdir, "-lm"],
+                   check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_plain_c_host_builds_and_links(tmp_path):
+    """A C caller compiles against include/ggs.h alone and links libggs.so; without
+    a GPU ggs_init reports GGS_ENODEV (exit 2) — the reference's device assert."""
+    import subprocess
+    exe = _build_c_host(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode in (0, 2), r.stdout + r.stderr
+    assert "ggs" in r.stdout
+
+
+@pytest.mark.gpu
+def test_plain_c_host_fused_fitness_matches_rendered_images(tmp_path):
+    import subprocess
+    exe = _build_c_host(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("candidate") == 4
