@@ -373,17 +373,21 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
                 GGS_BLEND(k, fu_);                                                      \
                 goto done;                                                              \
             }                                                                           \
-            if (rowb < y0 - 8 * (k)) fu_.x = 0.0f;          /* rows above y0 */         \
-            if (rowb < y0 - 8 * (k) - 4) fu_.y = 0.0f;                                  \
+            /* scalar row limits (readfirstlane keeps them off the VALU) */             \
+            if (rowb < ufirst(y0 - 8 * (k))) fu_.x = 0.0f;  /* rows above y0 */         \
+            if (rowb < ufirst(y0 - 8 * (k) - 4)) fu_.y = 0.0f;                          \
             GGS_BLEND(k, fu_);                                                          \
-            /* guard on the seed's bits (f >= 0: unsigned order = float order)  */      \
-            if (__ballot(inx) & __ballot((__float_as_uint(F2.x) < 0x0D800000u) |       \
-                                         (__float_as_uint(F2.y) < 0x0D800000u)))        \
+            /* guard on the seed's bits (f >= 0: unsigned order = float order);  */     \
+            /* dead lanes (px = -inf) excluded                                    */     \
+            if (__ballot((px > -__builtin_inff()) &                                     \
+                         (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u))) \
                 goto x##k;                                                              \
-            const float t8_ = __builtin_fmaf(bx, 8.0f, s.c64);                          \
-            f2_t d_ = fma2(qy_, (f2_t)s.c16, (f2_t)t8_);                                \
-            R2.x = GGS_EXP2(fminf(d_.x, 100.0f));                                       \
-            R2.y = GGS_EXP2(fminf(d_.y, 100.0f));                                       \
+            /* live lanes: d <= -e(seed) <= 100; dead lanes: d = -inf -> r = 0   */     \
+            const float t8_ = px > -__builtin_inff() ? __builtin_fmaf(bx, 8.0f, s.c64)  \
+                                                     : -__builtin_inff();               \
+            const f2_t d_ = fma2(qy_, (f2_t)s.c16, (f2_t)t8_);                          \
+            R2.x = GGS_EXP2(d_.x);                                                      \
+            R2.y = GGS_EXP2(d_.y);                                                      \
             goto u##k;                                                                  \
         }                                                                               \
         break;
@@ -419,8 +423,8 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     case k:                                                                             \
         if (k < NPK) {                                                                  \
             f2_t fu_ = F2 * R2;                                                         \
-            if (rowb > y1 - 8 * (k)) fu_.x = 0.0f;          /* rows below y1 */         \
-            if (rowb > y1 - 8 * (k) - 4) fu_.y = 0.0f;                                  \
+            if (rowb > ufirst(y1 - 8 * (k))) fu_.x = 0.0f;  /* rows below y1 */         \
+            if (rowb > ufirst(y1 - 8 * (k) - 4)) fu_.y = 0.0f;                          \
             GGS_BLEND(k, fu_);                                                          \
         }                                                                               \
         break;
