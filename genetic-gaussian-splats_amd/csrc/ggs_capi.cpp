@@ -901,27 +901,60 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     return GGS_OK;
 }
 
+// The SA state keeps, besides the current genome, its splat records and its
+// per-strip partials: a neighbour is then evaluated incrementally — only the
+// strips a changed splat (old or new AABB) touches are rasterised, the others
+// keep the current partial (bit-identical to a full evaluation: same cull list,
+// same blend order).  annealing.py:121-146 re-renders the whole canvas per try.
 struct SaSession {
     uint64_t plan_id = new_plan_id();
     DevCtx* c = nullptr;
     hipStream_t st = nullptr;
     ggs_ga_config cfg{};
-    int N = 0, cap = 0, last_n = 0;
+    int N = 0, cap = 0, last_n = 0, nTiles = 0;
+    bool incremental = false;   // measured slower at every SA config tried
     DevBuf curr, best, nb, nb_fits, target, mask, draws;
-    float* h_fits = nullptr;   // pinned
+    DevBuf cur_recs, nb_recs, cur_part, nb_part, dirty, plan, wpart, order, counters;
+    float* h_fits = nullptr;        // pinned
+    unsigned* h_counters = nullptr; // pinned: [0] changed splats (last propose)
+    uint64_t n_changed = 0, n_proposed = 0;
 };
 
 void sa_free(SaSession* s) {
-    for (DevBuf* b : {&s->curr, &s->best, &s->nb, &s->nb_fits, &s->target, &s->mask, &s->draws})
+    for (DevBuf* b : {&s->curr, &s->best, &s->nb, &s->nb_fits, &s->target, &s->mask, &s->draws,
+                      &s->cur_recs, &s->nb_recs, &s->cur_part, &s->nb_part, &s->dirty, &s->plan,
+                      &s->wpart, &s->order, &s->counters})
         if (b->p) (void)hipFree(b->p);
     if (s->h_fits) (void)hipHostFree(s->h_fits);
+    if (s->h_counters) (void)hipHostFree(s->h_counters);
     if (s->st) (void)hipStreamDestroy(s->st);
 }
 
-int sa_eval(SaSession* s, const float* G, int n, float* dev_out) {
-    return run_fitness(s->c, s->st, G, n, s->N, 9, (const float*)s->target.p,
-                       s->mask.p ? (const float*)s->mask.p : nullptr, s->cfg.fitness_mode,
-                       s->cfg.boost_beta, s->cfg.H, s->cfg.W, s->cfg.k_sigma, dev_out, s->plan_id);
+// prep -> [dirty] -> raster -> finalize for n genomes G; records / partials / fitness
+// land in recs / part / fits.  dirty != null: incremental against the current state.
+int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, float* part, float* fits, bool dirty) {
+    const ggs_ga_config& c = s->cfg;
+    {
+        ProfScope ps(s->st, 0);
+        GGS_HIP(launch_prep(s->st, true, G, (int64_t)n * s->N, 9, c.H, c.W, c.k_sigma, recs, nullptr,
+                            nullptr, nullptr));
+    }
+    if (dirty)
+        GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, G, (const SplatRec*)s->cur_recs.p, recs, n,
+                             s->N, c.H, c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p));
+    const float bg[3] = {1.f, 1.f, 1.f};
+    {
+        ProfScope ps(s->st, 1);
+        GGS_HIP(launch_raster(s->st, 1, recs, n, s->N, c.H, c.W, bg, nullptr, (const float4*)s->plan.p, part,
+                              (const int*)s->order.p, dirty ? (const unsigned char*)s->dirty.p : nullptr,
+                              (const float*)s->cur_part.p));
+    }
+    {
+        ProfScope ps(s->st, 2);
+        GGS_HIP(launch_finalize(s->st, part, (const float*)s->wpart.p, n, s->nTiles, c.fitness_mode, c.H, c.W,
+                                fits));
+    }
+    return GGS_OK;
 }
 
 // Shared validation of ggs_ga_create / ggs_sa_create.
@@ -1082,20 +1115,41 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     auto bail = [&](int code) { sa_free(s.get()); return code; };
     if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(GGS_EHIP, "stream creation failed"));
+    int nTX;
+    s->nTiles = raster_tiles(cfg->H, cfg->W, &nTX);
+    const size_t slots = 4 * (size_t)s->nTiles, rb = sizeof(SplatRec) * (size_t)std::max(s->N, 1);
     if ((rc = ensure(s->curr, std::max<size_t>(ib, 4), s->st)) || (rc = ensure(s->best, std::max<size_t>(ib, 4), s->st)) ||
         (rc = ensure(s->nb, std::max<size_t>(ib * s->cap, 4), s->st)) ||
         (rc = ensure(s->nb_fits, sizeof(float) * s->cap, s->st)) ||
         (rc = ensure(s->target, sizeof(float) * 3 * hw, s->st)) ||
-        (mask_hw && (rc = ensure(s->mask, sizeof(float) * hw, s->st))))
+        (mask_hw && (rc = ensure(s->mask, sizeof(float) * hw, s->st))) ||
+        (rc = ensure(s->cur_recs, rb, s->st)) || (rc = ensure(s->nb_recs, rb * s->cap, s->st)) ||
+        (rc = ensure(s->cur_part, sizeof(float) * slots, s->st)) ||
+        (rc = ensure(s->nb_part, sizeof(float) * slots * s->cap, s->st)) ||
+        (rc = ensure(s->dirty, slots * s->cap, s->st)) || (rc = ensure(s->plan, plan_bytes(cfg->H, cfg->W), s->st)) ||
+        (rc = ensure(s->wpart, sizeof(float) * slots, s->st)) ||
+        (rc = ensure(s->order, sizeof(int) * (size_t)s->nTiles, s->st)) ||
+        (rc = ensure(s->counters, sizeof(unsigned) * 4, s->st)))
         return bail(rc);
-    if (hipHostMalloc((void**)&s->h_fits, sizeof(float) * s->cap, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&s->h_fits, sizeof(float) * s->cap, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&s->h_counters, sizeof(unsigned) * 4, hipHostMallocDefault) != hipSuccess)
         return bail(fail(GGS_ENOMEM, "pinned allocation failed"));
+    std::vector<int> order(s->nTiles);
+    raster_tile_order(cfg->H, cfg->W, order.data());
     if (hipMemcpyAsync(s->target.p, target_hw3, sizeof(float) * 3 * hw, hipMemcpyHostToDevice, s->st) ||
         (mask_hw && hipMemcpyAsync(s->mask.p, mask_hw, sizeof(float) * hw, hipMemcpyHostToDevice, s->st)) ||
         hipMemcpyAsync(s->curr.p, init_ind, ib, hipMemcpyHostToDevice, s->st) ||
-        hipMemcpyAsync(s->best.p, init_ind, ib, hipMemcpyHostToDevice, s->st))
+        hipMemcpyAsync(s->best.p, init_ind, ib, hipMemcpyHostToDevice, s->st) ||
+        hipMemcpyAsync(s->order.p, order.data(), sizeof(int) * s->nTiles, hipMemcpyHostToDevice, s->st) ||
+        hipMemsetAsync(s->counters.p, 0, sizeof(unsigned) * 4, s->st))
         return bail(fail(GGS_EHIP, "upload failed"));
-    if ((rc = sa_eval(s.get(), (const float*)s->curr.p, 1, (float*)s->nb_fits.p))) return bail(rc);
+    if (launch_plan(s->st, (const float*)s->target.p, mask_hw ? (const float*)s->mask.p : nullptr,
+                    cfg->fitness_mode, cfg->boost_beta, cfg->H, cfg->W, (float4*)s->plan.p,
+                    (float*)s->wpart.p) != hipSuccess)
+        return bail(fail(GGS_EHIP, "plan launch failed"));
+    if ((rc = sa_eval(s.get(), (const float*)s->curr.p, 1, (SplatRec*)s->cur_recs.p, (float*)s->cur_part.p,
+                      (float*)s->nb_fits.p, false)))
+        return bail(rc);
     if (hipMemcpyAsync(s->h_fits, s->nb_fits.p, sizeof(float), hipMemcpyDeviceToHost, s->st) ||
         hipStreamSynchronize(s->st))
         return bail(fail(GGS_EHIP, "initial evaluation failed"));
@@ -1120,10 +1174,16 @@ int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_
     prm.o_base = first_try;
     GGS_HIP(launch_ga_variation(s->st, (const float*)s->curr.p, nullptr, 1, s->N, prm, d, s->cfg.seed, it,
                                 (float*)s->nb.p, n));
-    if ((rc = sa_eval(s, (const float*)s->nb.p, n, (float*)s->nb_fits.p))) return rc;
+    if ((rc = sa_eval(s, (const float*)s->nb.p, n, (SplatRec*)s->nb_recs.p, (float*)s->nb_part.p,
+                      (float*)s->nb_fits.p, s->incremental)))
+        return rc;
     GGS_HIP(hipMemcpyAsync(s->h_fits, s->nb_fits.p, sizeof(float) * n, hipMemcpyDeviceToHost, s->st));
+    GGS_HIP(hipMemcpyAsync(s->h_counters, s->counters.p, sizeof(unsigned), hipMemcpyDeviceToHost, s->st));
+    GGS_HIP(hipMemsetAsync(s->counters.p, 0, sizeof(unsigned), s->st));
     GGS_HIP(hipStreamSynchronize(s->st));
     memcpy(fits_out, s->h_fits, sizeof(float) * n);
+    s->n_changed += s->h_counters[0];
+    s->n_proposed += (uint64_t)n;
     s->last_n = n;
     return GGS_OK;
 }
@@ -1135,9 +1195,32 @@ int ggs_sa_commit(void* handle, int32_t j, int32_t update_best) {
     std::lock_guard<std::mutex> lk(s->c->mu);
     DeviceGuard dg(s->c->dev);
     const size_t ib = sizeof(float) * 9 * (size_t)s->N;
-    if (j >= 0)
+    if (j >= 0) {   // the accepted neighbour becomes the state: genome, records, strip partials
+        const size_t rb = sizeof(SplatRec) * (size_t)s->N, pb = sizeof(float) * 4 * (size_t)s->nTiles;
         GGS_HIP(hipMemcpyAsync(s->curr.p, (const char*)s->nb.p + ib * j, ib, hipMemcpyDeviceToDevice, s->st));
+        GGS_HIP(hipMemcpyAsync(s->cur_recs.p, (const char*)s->nb_recs.p + rb * j, rb, hipMemcpyDeviceToDevice,
+                               s->st));
+        GGS_HIP(hipMemcpyAsync(s->cur_part.p, (const char*)s->nb_part.p + pb * j, pb, hipMemcpyDeviceToDevice,
+                               s->st));
+    }
     if (update_best) GGS_HIP(hipMemcpyAsync(s->best.p, s->curr.p, ib, hipMemcpyDeviceToDevice, s->st));
+    return GGS_OK;
+}
+
+int ggs_sa_set_incremental(void* handle, int32_t on) {
+    if (!handle) return fail(GGS_EINVAL, "null handle");
+    SaSession* s = (SaSession*)handle;
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    s->incremental = on != 0;
+    return GGS_OK;
+}
+
+int ggs_sa_stats(void* handle, uint64_t* proposed, uint64_t* changed_splats) {
+    if (!handle) return fail(GGS_EINVAL, "null handle");
+    SaSession* s = (SaSession*)handle;
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    if (proposed) *proposed = s->n_proposed;
+    if (changed_splats) *changed_splats = s->n_changed;
     return GGS_OK;
 }
 

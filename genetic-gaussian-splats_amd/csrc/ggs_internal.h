@@ -26,7 +26,13 @@ hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_
 int raster_tiles(int H, int W, int* nTX);
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
-                         const int* tile_order);
+                         const int* tile_order, const unsigned char* dirty = nullptr,
+                         const float* clean = nullptr);
+// Strips touched by splats that differ between `nb` [n][N][9] and `curr` [N][9]
+// (old AABB from cur_recs, new from nb_recs) -> dirty [n][tiles][4] (zeroed first).
+hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, const SplatRec* cur_recs,
+                        const SplatRec* nb_recs, int n, int N, int H, int W, unsigned char* dirty,
+                        unsigned* n_changed);
 // Target plan for the fitness epilogue (built once per target/mask/mode/beta).
 hipError_t launch_plan(hipStream_t st, const float* target, const float* mask, int mode, float beta,
                        int H, int W, float4* plan, float* wpartials);

@@ -268,7 +268,8 @@ __global__ void __launch_bounds__(NT, GGS_OCC)
 raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
-              const int* __restrict__ tile_order) {
+              const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
+              const float* __restrict__ clean) {
     __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
     if (GGS_ABL == 6) {               // ablation: dispatch only
         if (threadIdx.x == 0 && partials) partials[blockIdx.x] = 0.0f;
@@ -284,6 +285,13 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     const int tx0 = (t % nTX) * TILE;
     const int ty0 = (t / nTX) * TILE_H;
     const int ty1 = min(ty0 + TILE_H, H) - 1;
+    if (MODE != 0 && dirty) {         // incremental (SA): a strip no changed splat touches
+        const int64_t slot = ((int64_t)b * nTiles + t) * 4 + wv;   // keeps the current state's
+        if (!dirty[slot]) {                                         // partial, bit for bit
+            if (lane == 0) partials[slot] = clean[t * 4 + wv];
+            return;
+        }
+    }
 
     const int sx0 = tx0 + wv * 16;    // this wave's strip: columns [sx0, sx0+15]
     const int col = sx0 + (lane & 15);
@@ -593,6 +601,51 @@ hipError_t launch_plan(hipStream_t st, const float* target, const float* mask, i
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// dirty strips (incremental SA evaluation, SURVEY.md §8f #4 / annealing.py:121-146)
+// ---------------------------------------------------------------------------
+// Thread per (neighbour b, splat i): if any of the 9 genes differ from the
+// current state (bitwise), every strip the splat's old or new AABB touches is
+// marked dirty for neighbour b.  Strips no changed splat touches keep their
+// cull list and blend order, so their partial is the current state's.
+__device__ __forceinline__ void mark_strips(const SplatRec& r, int nTX, unsigned char* __restrict__ d) {
+    for (int ty = r.y0 / TILE_H; ty <= r.y1 / TILE_H; ++ty)
+        for (int sx = r.x0 / 16; sx <= r.x1 / 16; ++sx) d[(ty * nTX + (sx >> 2)) * 4 + (sx & 3)] = 1;
+}
+
+__global__ void __launch_bounds__(256)
+dirty_kernel(const float* __restrict__ curr, const float* __restrict__ nb,
+             const SplatRec* __restrict__ cur_recs, const SplatRec* __restrict__ nb_recs, int n, int N,
+             int nTX, int nTiles, unsigned char* __restrict__ dirty, unsigned* __restrict__ n_changed) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)n * N) return;
+    const int b = (int)(idx / N), i = (int)(idx % N);
+    const unsigned* a = reinterpret_cast<const unsigned*>(curr + (int64_t)i * 9);
+    const unsigned* c = reinterpret_cast<const unsigned*>(nb + idx * 9);
+    unsigned diff = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) diff |= a[k] ^ c[k];
+    if (!diff) return;
+    unsigned char* d = dirty + (int64_t)b * nTiles * 4;
+    mark_strips(cur_recs[i], nTX, d);
+    mark_strips(nb_recs[idx], nTX, d);
+    if (n_changed) atomicAdd(n_changed, 1u);
+}
+
+hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, const SplatRec* cur_recs,
+                        const SplatRec* nb_recs, int n, int N, int H, int W, unsigned char* dirty,
+                        unsigned* n_changed) {
+    int nTX;
+    const int nTiles = raster_tiles(H, W, &nTX);
+    hipError_t e = hipMemsetAsync(dirty, 0, (size_t)n * nTiles * 4, st);
+    if (e != hipSuccess) return e;
+    const int64_t tot = (int64_t)n * N;
+    if (tot == 0) return hipSuccess;
+    hipLaunchKernelGGL(dirty_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, curr, nb,
+                       cur_recs, nb_recs, n, N, nTX, nTiles, dirty, n_changed);
+    return hipGetLastError();
+}
+
 size_t plan_bytes(int H, int W) { return sizeof(float4) * 4 * (size_t)raster_tiles(H, W, nullptr) * RG * 64; }
 
 // ---------------------------------------------------------------------------
@@ -693,13 +746,13 @@ int raster_tiles(int H, int W, int* nTX) {
 
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
-                         const int* tile_order) {
+                         const int* tile_order, const unsigned char* dirty, const float* clean) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
 #define GGS_RASTER(M)                                                                          \
     hipLaunchKernelGGL(raster_kernel<M>, grid, block, 0, st, recs, B, N, H, W, nTX, nTiles,     \
-                       bg[0], bg[1], bg[2], img, plan, partials, tile_order)
+                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean)
     if (mode == 0) GGS_RASTER(0);      // image
     else GGS_RASTER(1);                // fitness: the mode lives in the plan's weights
 #undef GGS_RASTER

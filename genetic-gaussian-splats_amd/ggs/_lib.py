@@ -82,6 +82,8 @@ SIGNATURES = {
     "ggs_sa_commit": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "ggs_sa_read": (C.c_int, [C.c_void_p, _f32p, _f32p, _f32p]),
     "ggs_sa_destroy": (None, [C.c_void_p]),
+    "ggs_sa_set_incremental": (C.c_int, [C.c_void_p, C.c_int32]),
+    "ggs_sa_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 
 

@@ -59,7 +59,7 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
                         evaluate: Optional[Callable[[np.ndarray], np.ndarray]] = None,
                         init_individual: Optional[np.ndarray] = None, progress: bool = True,
                         return_state: bool = False, speculate: Optional[int] = None,
-                        backend: str = "auto"):
+                        backend: str = "auto", incremental: bool = False):
     """annealing.py:47-190 → (best individual [N, 9] float32, best energy).
 
     Keyword-only hooks as ggs.ga.genetic_approx (``seed``, ``draws`` — a source
@@ -68,7 +68,12 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
     and ``backend``: "host" (numpy mutation + one libggs launch per batch),
     "device" (current state resident in HBM, mutation in-kernel: Philox keyed by
     (seed, iteration, try), or the explicit ``draws``; ggs/ga_device.DeviceSA) or
-    "auto" (device unless an ``evaluate`` hook is given)."""
+    "auto" (device unless an ``evaluate`` hook is given).  ``incremental``
+    (device backend): re-rasterise only the strips the changed splats touch
+    (bit-identical results; off by default — the double ``wrap_angle`` of
+    genetic.py:71 + utils.py:43 moves many θ by an ulp on every mutation, so
+    most strips are dirty anyway and the bookkeeping costs more than it saves,
+    DESIGN.md §9)."""
     from .mask import compute_importance_mask, prepare_target
     sched = temp_schedule
     t = prepare_target(target_img_uint8, H, W)                       # annealing.py:87
@@ -92,7 +97,7 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
     if backend == "device":
         prop = _DeviceProposer(t, imp_mask, curr, max(1, tries), mutpb, mut_sigma_max,
                                mut_sigma_min, sigma_schedule, min_scale_splats, max_scale_splats,
-                               k_sigma, boost_only, seed)
+                               k_sigma, boost_only, seed, incremental)
     elif backend == "host":
         prop = _HostProposer(curr, evaluate, iterations, sigma_schedule, mut_sigma_max,
                              mut_sigma_min, mutpb, H, W, min_scale_splats, max_scale_splats)
@@ -166,6 +171,7 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
             if hasattr(bar, "close"):
                 bar.close()
         best, curr = prop.best(), prop.current()
+        stats.update(prop.stats())
     finally:
         prop.close()
 
@@ -217,6 +223,9 @@ class _HostProposer:
     def current(self):
         return self.curr.copy()
 
+    def stats(self):
+        return {}
+
     def close(self):
         pass
 
@@ -225,14 +234,17 @@ class _DeviceProposer:
     """Neighbours mutated and evaluated on the GPU (ggs_sa_*)."""
 
     def __init__(self, t, mask, curr, max_tries, mutpb, sig_max, sig_min, schedule, min_s, max_s,
-                 k_sigma, boost_only, seed):
+                 k_sigma, boost_only, seed, incremental=False):
         from .ga_device import DeviceSA
         self.sa = DeviceSA(t, mask, curr, max_tries=max_tries, mutpb=mutpb, mut_sigma_max=sig_max,
                            mut_sigma_min=sig_min, schedule=schedule, min_scale_splats=min_s,
                            max_scale_splats=max_s, k_sigma=k_sigma, boost_only=boost_only,
                            seed=(int(np.random.SeedSequence().entropy) if seed is None
-                                 else int(seed)) & (2**64 - 1))
+                                 else int(seed)) & (2**64 - 1), incremental=incremental)
         self.init_fit = float(self.sa.init_fit)
+
+    def stats(self):
+        return self.sa.stats()
 
     def propose(self, it, total, first_try, w, d):
         return self.sa.propose(it, total, first_try, w, d)

@@ -65,7 +65,7 @@ class DeviceSA:
                  mut_sigma_max: Dict[str, float], mut_sigma_min: Dict[str, float],
                  schedule: str, min_scale_splats: float, max_scale_splats: float,
                  k_sigma: float = 3.0, boost_only: bool = False, boost_beta: float = 1.0,
-                 seed: int = 0, device: int = 0):
+                 seed: int = 0, device: int = 0, incremental: bool = False):
         ind = _arr(init_ind, np.float32)
         if ind.ndim != 2 or ind.shape[1] != 9:
             raise _lib.GGSInputError("the device SA keeps an [N, 9] genome")
@@ -84,6 +84,13 @@ class DeviceSA:
                                 ind.ctypes.data_as(_f32p), C.byref(h), C.byref(f)),
               "ggs_sa_create")
         self.h, self.init_fit, self.last_n = h, f.value, 0
+        check(lib.ggs_sa_set_incremental(h, int(bool(incremental))), "ggs_sa_set_incremental")
+
+    def stats(self) -> Dict[str, int]:
+        """Neighbours proposed and splats changed (the incremental path's work)."""
+        p, c = C.c_uint64(), C.c_uint64()
+        check(lib.ggs_sa_stats(self.h, C.byref(p), C.byref(c)), "ggs_sa_stats")
+        return {"proposed": p.value, "changed_splats": c.value}
 
     def propose(self, it: int, total: int, first_try: int, n: int, draws=None) -> np.ndarray:
         out = np.empty(n, np.float32)

@@ -187,6 +187,12 @@ int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_
 int ggs_sa_commit(void* handle, int32_t j, int32_t update_best);
 /* Synchronises; any output may be NULL.  neighbours: [n of the last propose][N][9]. */
 int ggs_sa_read(void* handle, float* current, float* best, float* neighbours);
+/* Incremental evaluation (default off): a neighbour's 16-column strips that no
+ * changed splat touches (old or new AABB) keep the current state's partial sums —
+ * bit-identical to a full re-render; off = every strip is rasterised. */
+int ggs_sa_set_incremental(void* handle, int32_t on);
+/* Neighbours proposed and splats found changed (summed over proposals). */
+int ggs_sa_stats(void* handle, uint64_t* proposed, uint64_t* changed_splats);
 void ggs_sa_destroy(void* handle);
 
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------

@@ -6,7 +6,8 @@ importance mask, initial evaluation — is timed separately and subtracted):
   reference's schedule);
 * host / speculative: numpy mutation, batched tries;
 * device / speculative: state resident in HBM, in-kernel mutation (Philox),
-  batched tries, one 4-byte-per-try readback per batch.
+  batched tries, one 4-byte-per-try readback per batch; "full" re-rasterises
+  every strip, "incremental" only the strips a changed splat touches.
 
 usage: python tools/bench_sa.py [--iters 20] [--size 2048] [--splats 4096] [--tries 8]"""
 import argparse, json, os, sys, time
@@ -43,13 +44,15 @@ def evaluate(G):
 
 
 res = {}
-for name, spec, backend in (("host_sequential", 1, "host"), ("host_speculative", None, "host"),
-                            ("device_speculative", None, "device")):
+for name, spec, backend, inc in (("host_sequential", 1, "host", False),
+                                 ("host_speculative", None, "host", False),
+                                 ("device_speculative_full", None, "device", False),
+                                 ("device_speculative_incremental", None, "device", True)):
     run = lambda n: A.simulated_annealing(          # noqa: E731
         target, H, W, "cuda", a.splats, a.mutpb, cfg["mut_sigma_max"], cfg["mut_sigma_min"],
         "cosine", 3.0, 0.1, 3.0, 0.7, False, n, 1e-3, "cosine", a.tries, seed=2,
         init_individual=init, evaluate=evaluate if backend == "host" else None, progress=False,
-        return_state=True, speculate=spec, backend=backend)
+        return_state=True, speculate=spec, backend=backend, incremental=inc)
     run(2)                                           # warm-up
     t0 = time.perf_counter()
     run(0)                                           # setup only
@@ -62,7 +65,11 @@ for name, spec, backend in (("host_sequential", 1, "host"), ("host_speculative",
                  "setup_ms": round(t_setup * 1e3, 1),
                  "eval_ms_per_iter": round(ev["s"] / a.iters * 1e3, 2) if backend == "host" else None,
                  "launches": st["stats"]["launches"], "evaluated": st["stats"]["evaluated"],
+                 "changed_splats_per_neighbour": round(st["stats"]["changed_splats"] /
+                                                       max(1, st["stats"]["proposed"]), 1)
+                 if "changed_splats" in st["stats"] else None,
                  "best_fit": fit}
 assert res["host_sequential"]["best_fit"] == res["host_speculative"]["best_fit"]
+assert res["device_speculative_full"]["best_fit"] == res["device_speculative_incremental"]["best_fit"]
 print(json.dumps({"metric": "SA iterations/s", "config": {"H": H, "W": W, "splats": a.splats,
                   "tries_per_iter": a.tries, "mutpb": a.mutpb, "iters": a.iters}, **res}))
