@@ -101,9 +101,13 @@ def cpu_baseline(tgt, mask, per_worker=80):
         pool.map(_cpu_worker, [(p, tgt, mask) for p in pops])
         dt = time.perf_counter() - t0
     n = cores * per_worker
+    t1 = time.perf_counter()                                      # 1 core
+    _cpu_worker((pops[0][:8], tgt, mask))
+    one = 8 / (time.perf_counter() - t1)
     return {"value": n / dt, "unit": "candidate renders/s", "cores": cores, "kind": "port",
             "sample": f"{n} candidates ({per_worker} per process x {cores} processes, 1 thread each) "
-                      f"at 512x512/256 splats, weighted fitness, oracle/ggs_oracle.py numpy; {dt:.1f} s"}
+                      f"at 512x512/256 splats, weighted fitness, oracle/ggs_oracle.py numpy; {dt:.1f} s",
+            "single_core_value": round(one, 2)}
 
 
 def main():
