@@ -294,8 +294,30 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
 // ---------------------------------------------------------------------------
 // survivors: elites by stable fitness order, next fitness vector, best, curves
 // ---------------------------------------------------------------------------
-constexpr int ST = 1024;   // one workgroup; bitonic sort of up to 4096 keys in LDS
+constexpr int ST = 1024;   // max threads; the launch uses min(ST, pow2 >= P) (cheap barriers at P=128)
 constexpr int SMAX = 4096;
+
+// bitonic sort of n2 (power of two) LDS keys (+ optional indices), ascending;
+// ties by index: lexicographic (key, idx) == Python's stable sorted()
+__device__ void bitonic(float* key, int* idx, int n2) {
+    const int nt = blockDim.x;
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = threadIdx.x; i < n2; i += nt) {
+                const int l = i ^ jj;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    const bool gt = key[i] > key[l] || (idx && key[i] == key[l] && idx[i] > idx[l]);
+                    if (gt == up) {
+                        const float tk = key[i]; key[i] = key[l]; key[l] = tk;
+                        if (idx) { const int ti = idx[i]; idx[i] = idx[l]; idx[l] = ti; }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
 
 __global__ void __launch_bounds__(ST)
 ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ off_fits, int P,
@@ -303,51 +325,43 @@ ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ of
                     GaBestDev best, double* __restrict__ curves_row, int init) {
     __shared__ float key[SMAX];
     __shared__ int idx[SMAX];
-    const int tid = threadIdx.x;
+    __shared__ float nf[SMAX];           // the next generation's fitness vector
+    const int tid = threadIdx.x, nt = blockDim.x;
     int n2 = 1;
     while (n2 < P) n2 <<= 1;
     if (!init) {
-        for (int i = tid; i < n2; i += ST) {
+        for (int i = tid; i < n2; i += nt) {
             key[i] = i < P ? fits[i] : __builtin_inff();
             idx[i] = i < P ? i : 0x7fffffff;
         }
         __syncthreads();
-        // bitonic sort on (key, idx): lexicographic == Python's stable sorted()
-        for (int k = 2; k <= n2; k <<= 1) {
-            for (int jj = k >> 1; jj > 0; jj >>= 1) {
-                for (int i = tid; i < n2; i += ST) {
-                    const int l = i ^ jj;
-                    if (l > i) {
-                        const bool up = (i & k) == 0;
-                        const bool gt = key[i] > key[l] || (key[i] == key[l] && idx[i] > idx[l]);
-                        if (gt == up) {
-                            const float tk = key[i]; key[i] = key[l]; key[l] = tk;
-                            const int ti = idx[i]; idx[i] = idx[l]; idx[l] = ti;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
+        bitonic(key, idx, n2);
         const int E = elite_k < 1 ? 1 : elite_k;                  // algorithm.py:129
-        for (int r = tid; r < P; r += ST) {
+        for (int r = tid; r < P; r += nt) {
+            float f;
             if (r < E) {
                 src[r] = idx[r];                                  // from the parents
-                new_fits[r] = fits[idx[r]];
+                f = key[r];
             } else {
                 src[r] = P + (r - E);                             // offspring r - E
-                new_fits[r] = off_fits[r - E];
+                f = off_fits[r - E];
             }
+            new_fits[r] = f;
+            nf[r] = f;
         }
-        __syncthreads();
+    } else {
+        for (int r = tid; r < P; r += nt) nf[r] = fits[r];
     }
-    const float* __restrict__ F = init ? fits : new_fits;
+    __syncthreads();
     // best so far (algorithm.py:64-67, 143-150) and curves (:71-75, 153-155)
     if (tid == 0) {
         int g = 0;
-        for (int r = 1; r < P; ++r)
-            if (F[r] < F[g]) g = r;
-        const double fg = (double)F[g];
+        double sum = (double)nf[0];                               // sum(fitnesses) / len, in order
+        for (int r = 1; r < P; ++r) {
+            if (nf[r] < nf[g]) g = r;
+            sum += (double)nf[r];
+        }
+        const double fg = (double)nf[g];
         if (init || fg + 1e-10 < *best.fit) {
             *best.fit = fg;
             *best.src = init ? g : src[g];
@@ -355,28 +369,13 @@ ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ of
         } else {
             *best.updated = 0;
         }
-        double sum = 0.0;                                         // sum(fitnesses) / len
-        for (int r = 0; r < P; ++r) sum += (double)F[r];
         curves_row[0] = *best.fit;
         curves_row[1] = sum / (double)P;
     }
     // median: sort the new fitness values (statistics.median on the list)
-    for (int i = tid; i < n2; i += ST) key[i] = i < P ? F[i] : __builtin_inff();
+    for (int i = tid; i < n2; i += nt) key[i] = i < P ? nf[i] : __builtin_inff();
     __syncthreads();
-    for (int k = 2; k <= n2; k <<= 1) {
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-            for (int i = tid; i < n2; i += ST) {
-                const int l = i ^ jj;
-                if (l > i) {
-                    const bool up = (i & k) == 0;
-                    if ((key[i] > key[l]) == up) {
-                        const float t = key[i]; key[i] = key[l]; key[l] = t;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
+    bitonic(key, nullptr, n2);
     if (tid == 0)
         curves_row[2] = (P & 1) ? (double)key[P / 2] : ((double)key[P / 2 - 1] + (double)key[P / 2]) / 2.0;
 }
@@ -408,7 +407,9 @@ hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fi
 hipError_t launch_ga_survivors(hipStream_t st, const float* fits, const float* off_fits, int P,
                                int elite_k, int* src, float* new_fits, const GaBestDev& best,
                                double* curves_row, int init) {
-    hipLaunchKernelGGL(ga_survivors_kernel, dim3(1), dim3(ST), 0, st, fits, off_fits, P, elite_k,
+    int nt = 64;
+    while (nt < P && nt < ST) nt <<= 1;
+    hipLaunchKernelGGL(ga_survivors_kernel, dim3(1), dim3(nt), 0, st, fits, off_fits, P, elite_k,
                        src, new_fits, best, curves_row, init);
     return hipGetLastError();
 }
