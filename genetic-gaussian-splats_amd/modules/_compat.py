@@ -37,3 +37,30 @@ def check_device(device) -> None:
     kind = getattr(device, "type", None) or str(device).split(":")[0]
     if kind != "cuda":
         raise ggs.GGSInputError("This renderer requires a CUDA device.")
+
+
+def hip_device_of(*xs):
+    """Device index when every x is a torch tensor on the same HIP ("cuda")
+    device, else None: such inputs take the device-pointer path (no PCIe copy)."""
+    dev = None
+    for x in xs:
+        if x is None:
+            continue
+        if not is_torch(x) or x.device.type != "cuda":
+            return None
+        idx = x.device.index if x.device.index is not None else \
+            sys.modules["torch"].cuda.current_device()
+        if dev is not None and idx != dev:
+            return None
+        dev = idx
+    return dev
+
+
+def f32_contig(x):
+    """torch tensor -> contiguous float32 (same device)."""
+    torch = sys.modules["torch"]
+    return x.detach().to(torch.float32).contiguous()
+
+
+def stream_of(dev: int) -> int:
+    return sys.modules["torch"].cuda.current_stream(dev).cuda_stream

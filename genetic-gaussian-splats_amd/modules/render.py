@@ -9,7 +9,9 @@ reference caller) is accepted; the canvas is always float32.
 """
 from __future__ import annotations
 
-from modules._compat import check_device, ggs, like
+import sys
+
+from modules._compat import check_device, f32_contig, ggs, hip_device_of, like, stream_of
 
 _DEV = "cuda"   # imported by run_ggs.py:8 / run_sags.py:8; 'cuda' is ROCm's HIP device type
 __all__ = ["render_splats_rgb_triton", "_DEV"]
@@ -21,5 +23,18 @@ def render_splats_rgb_triton(genomes, H: int, W: int, *, k_sigma: float = 3.0, d
     """render.py:203-252 → [B,H,W,3] float32 clamped to [0,1] (numpy, or torch
     on the input's device when given a torch tensor)."""
     check_device(device or _DEV)
+    dev = hip_device_of(genomes)
+    if dev is not None:                   # torch tensor on the GPU: device pointers, no copies
+        torch = sys.modules["torch"]
+        if genomes.ndim not in (2, 3):
+            raise ggs.GGSInputError("Expected genomes [N,C] or [B,N,C]")   # render.py:219
+        g = f32_contig(genomes if genomes.ndim == 3 else genomes.unsqueeze(0))
+        B, N, C = g.shape
+        if C < 9:
+            raise ggs.GGSInputError("Expected at least 9 genome cols")    # render.py:223
+        out = torch.empty((B, H, W, 3), dtype=torch.float32, device=g.device)
+        ggs.render_device(dev, stream_of(dev), g.data_ptr(), B, N, C, H, W, k_sigma,
+                          out.data_ptr(), background=background)
+        return out
     out = ggs.render(genomes, H, W, k_sigma=k_sigma, background=background)
     return like(out, genomes)

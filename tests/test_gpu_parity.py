@@ -350,6 +350,18 @@ def test_drop_in_modules_numpy_and_torch():
     assert isinstance(img, torch.Tensor) and img.shape == (len(pop), H, W, 3)
     with pytest.raises(AssertionError):
         render_splats_rgb_triton(g9, H, W, device="cpu")
+    # the torch-on-GPU path (device pointers, no host copies) gives the host path's bits
+    g9h = genome_to_renderer_batched(pop)
+    np.testing.assert_array_equal(img.cpu().numpy(), render_splats_rgb_triton(g9h, H, W))
+    one = render_splats_rgb_triton(g9[1].double().t().contiguous().t(), H, W)   # 2-D, f64, strided
+    np.testing.assert_array_equal(one[0].cpu().numpy(), render_splats_rgb_triton(g9h[1], H, W)[0])
+    for kw in ({}, {"weight_mask": mask}, {"weight_mask": mask, "boost_only": True}):
+        host = fitness_many(list(pop), tgt, H, W, 3.0, "cuda", **kw)
+        kwt = {k: (torch.from_numpy(v).cuda() if isinstance(v, np.ndarray) else v) for k, v in kw.items()}
+        dev = fitness_many(tp, torch.from_numpy(tgt).cuda(), H, W, 3.0, "cuda", **kwt)
+        np.testing.assert_array_equal(dev.cpu().numpy(), host)
+        lst = fitness_population(tp, torch.from_numpy(tgt).cuda(), H, W, 3.0, "cuda", chunk=3, **kwt)
+        assert lst == host.tolist()
 
 
 # ---- GA layer on the GPU evaluator (§8f next #1) ----------------------------------------------
