@@ -107,7 +107,18 @@ def cpu_baseline(tgt, mask, per_worker=80):
     return {"value": n / dt, "unit": "candidate renders/s", "cores": cores, "kind": "port",
             "sample": f"{n} candidates ({per_worker} per process x {cores} processes, 1 thread each) "
                       f"at 512x512/256 splats, weighted fitness, oracle/ggs_oracle.py numpy; {dt:.1f} s",
-            "single_core_value": round(one, 2)}
+            "single_core_value": round(one, 2), "cpu_model": _cpu_model(),
+            "host_cpus_visible": os.cpu_count()}
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
