@@ -296,6 +296,7 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
 // ---------------------------------------------------------------------------
 constexpr int ST = 1024;   // max threads; the launch uses min(ST, pow2 >= P) (cheap barriers at P=128)
 constexpr int SMAX = 4096;
+constexpr int RANKMAX = 512;   // counting ranks below this population size
 
 // bitonic sort of n2 (power of two) LDS keys (+ optional indices), ascending;
 // ties by index: lexicographic (key, idx) == Python's stable sorted()
@@ -327,6 +328,65 @@ ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ of
     __shared__ int idx[SMAX];
     __shared__ float nf[SMAX];           // the next generation's fitness vector
     const int tid = threadIdx.x, nt = blockDim.x;
+    const int E = elite_k < 1 ? 1 : elite_k;                      // algorithm.py:129
+    if (P <= RANKMAX) {
+        // Small populations: ranks by counting (one LDS pass per element, 3
+        // barriers) instead of two bitonic sorts (~60 barriers).  rank(r) = #{j:
+        // (f_j, j) < (f_r, r)} is the position in Python's stable sorted().
+        __shared__ float med[2];
+        for (int r = tid; r < P; r += nt) key[r] = fits[r];
+        __syncthreads();
+        if (!init) {
+            for (int r = tid; r < P; r += nt) {
+                const float f = key[r];
+                int rank = 0;
+                for (int j = 0; j < P; ++j) rank += (key[j] < f) | ((key[j] == f) & (j < r));
+                if (rank < E) {                                   // an elite, from the parents
+                    src[rank] = r;
+                    new_fits[rank] = f;
+                    nf[rank] = f;
+                }
+            }
+            for (int r = E + tid; r < P; r += nt) {               // offspring r - E
+                const float f = off_fits[r - E];
+                src[r] = P + (r - E);
+                new_fits[r] = f;
+                nf[r] = f;
+            }
+        } else {
+            for (int r = tid; r < P; r += nt) nf[r] = key[r];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int g = 0;
+            double sum = (double)nf[0];                           // sum(fitnesses) / len, in order
+            for (int r = 1; r < P; ++r) {
+                if (nf[r] < nf[g]) g = r;
+                sum += (double)nf[r];
+            }
+            const double fg = (double)nf[g];
+            if (init || fg + 1e-10 < *best.fit) {
+                *best.fit = fg;
+                *best.src = init ? g : src[g];
+                *best.updated = 1;
+            } else {
+                *best.updated = 0;
+            }
+            curves_row[0] = *best.fit;
+            curves_row[1] = sum / (double)P;
+        }
+        for (int r = tid; r < P; r += nt) {                       // statistics.median
+            const float f = nf[r];
+            int rank = 0;
+            for (int j = 0; j < P; ++j) rank += (nf[j] < f) | ((nf[j] == f) & (j < r));
+            if (rank == P / 2) med[1] = f;
+            if (rank == P / 2 - 1) med[0] = f;
+        }
+        __syncthreads();
+        if (tid == 0)
+            curves_row[2] = (P & 1) ? (double)med[1] : ((double)med[0] + (double)med[1]) / 2.0;
+        return;
+    }
     int n2 = 1;
     while (n2 < P) n2 <<= 1;
     if (!init) {
@@ -336,7 +396,6 @@ ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ of
         }
         __syncthreads();
         bitonic(key, idx, n2);
-        const int E = elite_k < 1 ? 1 : elite_k;                  // algorithm.py:129
         for (int r = tid; r < P; r += nt) {
             float f;
             if (r < E) {

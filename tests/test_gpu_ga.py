@@ -42,6 +42,7 @@ def _problem(H, W, seed):
     (64, 48, 32, 300, 3, 2, 8, 0.9, 0.05, True, 2),    # N > 256: multi-pass workgroup loops
     (32, 32, 8, 2, 5, 2, 1, 0.3, 0.01, False, 3),      # N = 2, rare mutation -> fallbacks
     (24, 24, 6, 1, 3, 2, 0, 0.5, 0.5, False, 4),       # N = 1: no swap; elite_k 0 -> 1
+    (16, 16, 600, 3, 2, 3, 25, 0.5, 0.1, False, 5),    # P > 512: bitonic survivors path
 ])
 def test_device_ga_matches_host_ga_with_same_draws(H, W, P, N, G, tour_k, elite_k, cxpb, mutpb,
                                                     boost, seed):
