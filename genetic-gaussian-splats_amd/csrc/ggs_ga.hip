@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "ggs_internal.h"
+#include "ggs_prep.h"
 
 namespace ggs {
 
@@ -96,7 +97,7 @@ constexpr int VT = 256;   // threads per variation workgroup
 __global__ void __launch_bounds__(VT)
 ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fits, int P, int N,
                     GaParamsDev prm, GaDrawsDev d, uint32_t k0, uint32_t k1, int gen,
-                    float* __restrict__ off) {
+                    float* __restrict__ off, SplatRec* __restrict__ recs, int H, int W, float k_sigma) {
     __shared__ int s_a, s_b, s_cx;
     __shared__ float s_sizei;
     __shared__ int s_j, s_count;
@@ -223,7 +224,7 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
 #pragma unroll
         for (int c = 0; c < 9; ++c) O[(int64_t)s * 9 + c] = g[c];
     }
-    if (N < 2) return;
+    if (N >= 2) {
     __syncthreads();   // workgroup-scope ordering of the rows just written
 
     // genetic.py:79-91: pick i, then the pick-th later splat bigger than i
@@ -253,7 +254,7 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
         __syncthreads();
     }
     const int count = s_count;
-    if (count == 0) return;
+    if (count > 0) {
     int pick;
     if (d.swap_pick && d.swap_pick[o] >= 0) pick = d.swap_pick[o];
     else {
@@ -289,6 +290,16 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
         O[(int64_t)i * 9 + tid] = b;
         O[(int64_t)j * 9 + tid] = a;
     }
+    }   // count > 0
+    }   // N >= 2
+    if (recs) {             // prep fused in (ggs_prep.h): the raster's records of this offspring
+        __syncthreads();    // swapped rows visible to the workgroup
+        for (int s = tid; s < N; s += VT) {
+            float row[9];
+            encode_row(O + (int64_t)s * 9, row);
+            recs[(int64_t)o * N + s] = make_rec(preprocess_row(row, H, W, k_sigma));
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -323,10 +334,32 @@ __device__ void bitonic(float* key, int* idx, int n2) {
 __global__ void __launch_bounds__(ST)
 ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ off_fits, int P,
                     int elite_k, int* __restrict__ src, float* __restrict__ new_fits,
-                    GaBestDev best, double* __restrict__ curves_row, int init) {
+                    GaBestDev best, double* __restrict__ curves_row, int init, FitReduce fr) {
+    // The surviving offspring's fitness (rows E..P-1 of the next generation):
+    // given, or reduced here from the raster's strip partials, one wave per
+    // candidate (finalize_wave: the same bits as finalize_kernel).
+    const int E0 = elite_k < 1 ? 1 : elite_k;
+    __shared__ float nf[SMAX];           // the next generation's fitness vector
+    if (!init && fr.partials) {          // one wave per candidate
+        const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+        for (int q = wave; q < P - E0; q += nw) {
+            const float f = finalize_wave(fr.partials, fr.wpartials, fr.nT, fr.mode, fr.hw, q);
+            if ((threadIdx.x & 63) == 0) {
+                nf[E0 + q] = f;
+                new_fits[E0 + q] = f;
+                src[E0 + q] = P + q;                                // offspring q
+            }
+        }
+    } else if (!init) {                  // one thread per candidate
+        for (int q = threadIdx.x; q < P - E0; q += blockDim.x) {
+            const float f = off_fits[q];
+            nf[E0 + q] = f;
+            new_fits[E0 + q] = f;
+            src[E0 + q] = P + q;
+        }
+    }
     __shared__ float key[SMAX];
     __shared__ int idx[SMAX];
-    __shared__ float nf[SMAX];           // the next generation's fitness vector
     const int tid = threadIdx.x, nt = blockDim.x;
     const int E = elite_k < 1 ? 1 : elite_k;                      // algorithm.py:129
     if (P <= RANKMAX) {
@@ -347,12 +380,7 @@ ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ of
                     nf[rank] = f;
                 }
             }
-            for (int r = E + tid; r < P; r += nt) {               // offspring r - E
-                const float f = off_fits[r - E];
-                src[r] = P + (r - E);
-                new_fits[r] = f;
-                nf[r] = f;
-            }
+            // rows E..P-1 (the offspring) were written above
         } else {
             for (int r = tid; r < P; r += nt) nf[r] = key[r];
         }
@@ -396,17 +424,10 @@ ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ of
         }
         __syncthreads();
         bitonic(key, idx, n2);
-        for (int r = tid; r < P; r += nt) {
-            float f;
-            if (r < E) {
-                src[r] = idx[r];                                  // from the parents
-                f = key[r];
-            } else {
-                src[r] = P + (r - E);                             // offspring r - E
-                f = off_fits[r - E];
-            }
-            new_fits[r] = f;
-            nf[r] = f;
+        for (int r = tid; r < E; r += nt) {                       // the elites, from the parents
+            src[r] = idx[r];
+            new_fits[r] = key[r];
+            nf[r] = key[r];
         }
     } else {
         for (int r = tid; r < P; r += nt) nf[r] = fits[r];
@@ -457,19 +478,19 @@ ga_gather_kernel(const float* __restrict__ pop, const float* __restrict__ off, i
 // ---------------------------------------------------------------------------
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
-                               float* off, int n_off) {
+                               float* off, int n_off, SplatRec* recs, int H, int W, float k_sigma) {
     hipLaunchKernelGGL(ga_variation_kernel, dim3(n_off), dim3(VT), 0, st, pop, fits, P, N, prm, d,
-                       (uint32_t)seed, (uint32_t)(seed >> 32), gen, off);
+                       (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma);
     return hipGetLastError();
 }
 
 hipError_t launch_ga_survivors(hipStream_t st, const float* fits, const float* off_fits, int P,
                                int elite_k, int* src, float* new_fits, const GaBestDev& best,
-                               double* curves_row, int init) {
-    int nt = 64;
+                               double* curves_row, int init, const FitReduce& fr) {
+    int nt = fr.partials ? 512 : 64;   // 8 waves for the fused per-candidate reductions
     while (nt < P && nt < ST) nt <<= 1;
     hipLaunchKernelGGL(ga_survivors_kernel, dim3(1), dim3(nt), 0, st, fits, off_fits, P, elite_k,
-                       src, new_fits, best, curves_row, init);
+                       src, new_fits, best, curves_row, init, fr);
     return hipGetLastError();
 }
 

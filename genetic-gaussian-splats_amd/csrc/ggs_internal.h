@@ -77,10 +77,18 @@ struct GaBestDev {
 };
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
-                               float* off, int n_off);   // n_off offspring (GA: P; SA: tries)
+                               float* off, int n_off,    // n_off offspring (GA: P; SA: tries)
+                               SplatRec* recs = nullptr, int H = 0, int W = 0, float k_sigma = 3.0f);
+                               // recs != null: also prep the offspring (records [n_off][N])
+struct FitReduce {               // survivors reduces the offspring's strip partials itself
+    const float* partials = nullptr; // [P][nT] (null: use off_fits)
+    const float* wpartials = nullptr;
+    int nT = 0, mode = 0;
+    double hw = 0.0;
+};
 hipError_t launch_ga_survivors(hipStream_t st, const float* fits, const float* off_fits, int P,
                                int elite_k, int* src, float* new_fits, const GaBestDev& best,
-                               double* curves_row, int init);
+                               double* curves_row, int init, const FitReduce& fr = FitReduce{});
 hipError_t launch_ga_gather(hipStream_t st, const float* pop, const float* off, int P, int N,
                             const int* src, float* next, const GaBestDev& best, int init);
 int ga_max_population();

@@ -35,96 +35,15 @@
 
 #include "ggs_detmath.h"
 #include "ggs_internal.h"
+#include "ggs_prep.h"
 
 namespace ggs {
 
 using namespace detmath;
 
 // ---------------------------------------------------------------------------
-// prep
+// prep (per-splat math in ggs_prep.h, shared with the GA's fused variation)
 // ---------------------------------------------------------------------------
-struct Prep13 {
-    float cx, cy, sxx, sxy, syy, rc, gc, bc, a;
-    int x0, x1, y0, y1;
-};
-
-// encode.py:4-24 + 27-59: axes-angle row -> renderer row (g2, g3, g4 replaced,
-// colours/alpha clamped).  Same op order as oracle/ggs_oracle.py.
-__device__ __forceinline__ void encode_row(const float* __restrict__ g, float out[9]) {
-    const float sx = det_expf(g[2]);
-    const float sy = det_expf(g[3]);
-    float s, c;
-    det_sincosf(g[4], &s, &c);
-    const float sx2 = sx * sx, sy2 = sy * sy, c2 = c * c, s2 = s * s;
-    const float sxx = sx2 * c2 + sy2 * s2;
-    const float sxy = ((sx2 - sy2) * s) * c;
-    const float syy = sx2 * s2 + sy2 * c2;
-    const float l11 = ggs_sqrt_rn(nmax(sxx, EPS12));
-    const float l21 = ggs_div_rn(sxy, l11);
-    const float l22 = ggs_sqrt_rn(nmax(syy - l21 * l21, EPS12));
-    out[0] = g[0];
-    out[1] = g[1];
-    out[2] = det_logf(l11);
-    out[3] = det_logf(l22);
-    out[4] = l21;
-#pragma unroll
-    for (int j = 5; j < 9; ++j) out[j] = nclamp(g[j], 0.0f, 255.0f);
-}
-
-// render.py:8-47 on one renderer row.
-__device__ __forceinline__ Prep13 preprocess_row(const float g[9], int H, int W, float k) {
-    Prep13 p;
-    const float maxx = (float)(W - 1), maxy = (float)(H - 1);
-    p.cx = nclamp(g[0], 0.0f, 1.0f) * maxx;
-    p.cy = nclamp(g[1], 0.0f, 1.0f) * maxy;
-    const float l11 = nmax(det_expf(g[2]), EPS6);
-    const float l22 = nmax(det_expf(g[3]), EPS6);
-    const float l21 = g[4];
-    const float hx = nmax(k * fabsf(l11), 1.0f);
-    const float hy = nmax(k * (fabsf(l21) + fabsf(l22)), 1.0f);
-    p.x0 = (int)floorf(nclamp(p.cx - hx, 0.0f, maxx));
-    p.x1 = (int)ceilf(nclamp(p.cx + hx, 0.0f, maxx));
-    p.y0 = (int)floorf(nclamp(p.cy - hy, 0.0f, maxy));
-    p.y1 = (int)ceilf(nclamp(p.cy + hy, 0.0f, maxy));
-    const float i11 = ggs_div_rn(1.0f, l11);
-    const float i22 = ggs_div_rn(1.0f, l22);
-    const float i21 = (-l21) * (i11 * i22);
-    p.sxx = i11 * i11 + i21 * i21;
-    p.sxy = i21 * i22;
-    p.syy = i22 * i22;
-    p.rc = ggs_div_rn(nclamp(g[5], 0.0f, 255.0f), 255.0f);
-    p.gc = ggs_div_rn(nclamp(g[6], 0.0f, 255.0f), 255.0f);
-    p.bc = ggs_div_rn(nclamp(g[7], 0.0f, 255.0f), 255.0f);
-    p.a = ggs_div_rn(nclamp(g[8], 0.0f, 255.0f), 255.0f);
-    return p;
-}
-
-// Raster coefficients.  exp(-0.5*quad)*a == exp2(e) with
-// e = K*(sxx qx^2 + 2 sxy qx qy + syy qy^2) + log2(a),  K = -0.5*log2(e).
-__device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
-    constexpr float K = -0.72134752044448170f;
-    SplatRec r;
-    r.cx = p.cx;
-    r.cy = p.cy;
-    r.A = K * p.sxx;
-    r.Bc = 2.0f * K * p.sxy;
-    r.Cc = K * p.syy;
-    r.la = p.a > 0.0f ? __builtin_amdgcn_logf(p.a) : -__builtin_inff();
-    r.r = p.rc;
-    r.g = p.gc;
-    r.b = p.bc;
-    // f(qy + 8) = f(qy) * 2^d(qy),  d(qy) = e(qy + 8) - e(qy) = 16 Cc qy + 64 Cc + 8 bx,
-    // d(qy + 8) = d(qy) + 128 Cc  ->  the raster walks rows with two multiplies.
-    r.rho = __builtin_amdgcn_exp2f(128.0f * r.Cc);
-    r.c16 = 16.0f * r.Cc;
-    r.c64 = 64.0f * r.Cc;
-    r.x0 = p.x0;
-    r.x1 = p.x1;
-    r.y0 = p.y0;
-    r.y1 = p.y1;
-    return r;
-}
-
 template <bool ENCODE>
 __global__ void __launch_bounds__(256)
 prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, float k,
@@ -653,31 +572,11 @@ size_t plan_bytes(int H, int W) { return sizeof(float4) * 4 * (size_t)raster_til
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 finalize_kernel(const float* __restrict__ partials, const float* __restrict__ wpartials,
-                int nTiles, int mode, double hw, float* __restrict__ out) {
-    __shared__ double sd[256];
-    __shared__ double sw[256];
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    double s = 0.0, w = 0.0;
-    for (int i = tid; i < nTiles; i += 256) {
-        s += (double)partials[(int64_t)b * nTiles + i];
-        if (mode != GGS_FIT_NONE) w += (double)wpartials[i];
-    }
-    sd[tid] = s;
-    sw[tid] = w;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) { sd[tid] += sd[tid + o]; sw[tid] += sw[tid + o]; }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        const double num = sd[0], wsum = sw[0];
-        double v;
-        if (mode == GGS_FIT_NONE) v = num / (3.0 * hw);                       // fitness.py:18-19
-        else if (mode == GGS_FIT_WEIGHTED) v = num / (wsum + 1e-12);          // fitness.py:28-31
-        else v = (num / (3.0 * hw)) / (wsum / hw + 1e-12);                    // fitness.py:23-27
-        out[b] = (float)v;
-    }
+                int nTiles, int mode, double hw, int B, float* __restrict__ out) {
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per candidate (ggs_prep.h)
+    if (b >= B) return;
+    const float v = finalize_wave(partials, wpartials, nTiles, mode, hw, b);
+    if ((threadIdx.x & 63) == 0) out[b] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -762,8 +661,8 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, 
 hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,
                            int nTiles, int mode, int H, int W, float* out) {
     // 4 strip partials per (candidate, tile)
-    hipLaunchKernelGGL(finalize_kernel, dim3(B), dim3(256), 0, st, partials, wpartials, nTiles * 4, mode,
-                       (double)H * (double)W, out);
+    hipLaunchKernelGGL(finalize_kernel, dim3((B + 3) / 4), dim3(256), 0, st, partials, wpartials, nTiles * 4,
+                       mode, (double)H * (double)W, B, out);
     return hipGetLastError();
 }
 
