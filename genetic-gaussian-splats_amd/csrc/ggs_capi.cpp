@@ -961,9 +961,10 @@ void sa_free(SaSession* s) {
 
 // prep -> [dirty] -> raster -> finalize for n genomes G; records / partials / fitness
 // land in recs / part / fits.  dirty != null: incremental against the current state.
-int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, float* part, float* fits, bool dirty) {
+int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, float* part, float* fits, bool dirty,
+            bool have_recs = false) {
     const ggs_ga_config& c = s->cfg;
-    {
+    if (!have_recs) {
         ProfScope ps(s->st, 0);
         GGS_HIP(launch_prep(s->st, true, G, (int64_t)n * s->N, 9, c.H, c.W, c.k_sigma, recs, nullptr,
                             nullptr, nullptr));
@@ -1215,10 +1216,14 @@ int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_
     GaParamsDev prm = ga_params(s->cfg, it, total_iters);
     prm.mutate_only = 1;
     prm.o_base = first_try;
-    GGS_HIP(launch_ga_variation(s->st, (const float*)s->curr.p, nullptr, 1, s->N, prm, d, s->cfg.seed, it,
-                                (float*)s->nb.p, n));
+    {   // the neighbours and their raster records (prep fused into the variation kernel)
+        ProfScope ps(s->st, 0);
+        GGS_HIP(launch_ga_variation(s->st, (const float*)s->curr.p, nullptr, 1, s->N, prm, d, s->cfg.seed, it,
+                                    (float*)s->nb.p, n, (SplatRec*)s->nb_recs.p, s->cfg.H, s->cfg.W,
+                                    s->cfg.k_sigma));
+    }
     if ((rc = sa_eval(s, (const float*)s->nb.p, n, (SplatRec*)s->nb_recs.p, (float*)s->nb_part.p,
-                      (float*)s->nb_fits.p, s->incremental)))
+                      (float*)s->nb_fits.p, s->incremental, true)))
         return rc;
     GGS_HIP(hipMemcpyAsync(s->h_fits, s->nb_fits.p, sizeof(float) * n, hipMemcpyDeviceToHost, s->st));
     GGS_HIP(hipMemcpyAsync(s->h_counters, s->counters.p, sizeof(unsigned), hipMemcpyDeviceToHost, s->st));
