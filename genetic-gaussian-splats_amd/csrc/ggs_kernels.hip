@@ -98,6 +98,28 @@ constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Row limits as wave lane masks.  Lane l owns row phase ph = l >> 4, so "the
+// lane's row in this pair is >= / <= a wave-uniform bound" is a contiguous range
+// of 16-lane blocks: built on the SALU (one 64-bit shift serves both rows of the
+// pair: s_lshl/s_lshr_b64 take the shift mod 64), applied by one v_cndmask with
+// an SGPR-pair condition — no per-lane compare.
+struct PairLanes { uint64_t x, y; };          // rows 8k+ph (x) and 8k+4+ph (y)
+// j = y0 - (ty0 + 8k) <= 7: keep lanes whose row >= y0 (ph >= j, ph + 4 >= j)
+__device__ __forceinline__ PairLanes rows_from(int j) {
+    const int jc = max(j, 0);
+    const uint64_t t = ~0ull << ((16 * jc) & 63);
+    return {jc < 4 ? t : 0ull, jc < 4 ? ~0ull : t};
+}
+// m = y1 - (ty0 + 8k) >= 0: keep lanes whose row <= y1 (ph <= m, ph + 4 <= m)
+__device__ __forceinline__ PairLanes rows_upto(int m) {
+    const int mc = min(m, 7);
+    const uint64_t u = ~0ull >> ((48 - 16 * mc) & 63);
+    return {mc >= 3 ? ~0ull : u, mc >= 4 ? u : 0ull};
+}
+__device__ __forceinline__ float keep_if(uint64_t lanes, float f) {
+    return __builtin_amdgcn_inverse_ballot_w64(lanes) ? f : 0.0f;
+}
+
 #define GGS_FOR16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
 // One (splat, row group) pair for this lane's pixel (col, ty0 + 4g + ph):
@@ -217,7 +239,6 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     const int ph = lane >> 4;         // row phase 0..3
     const float Xf = (float)col;
     const float Yb = (float)(ty0 + ph);
-    const int rowb = ty0 + ph;        // this lane's row in row group 0
 
     // 16 pixels per lane x (R, G, B, transmittance), as named scalars: arrays
     // get vectorised into <16 x float> values whose phis the allocator splits.
@@ -293,16 +314,17 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             const f2_t e_ = fma2(qy_, fma2(Cc2, qy_, bx2), px2);                        \
             F2.x = GGS_EXP2(e_.x);                                                      \
             F2.y = GGS_EXP2(e_.y);                                                      \
-            f2_t fu_ = F2;                                                              \
+            f2_t fu_;                                                                   \
+            const PairLanes top_ = rows_from(y0 - ty0 - 8 * (k));                       \
             if (kB == k) {                /* one pair: both AABB row limits */          \
-                if ((unsigned)(8 * (k) - rlo) > rspan) fu_.x = 0.0f;                    \
-                if ((unsigned)(8 * (k) + 4 - rlo) > rspan) fu_.y = 0.0f;                \
+                const PairLanes bot_ = rows_upto(y1 - ty0 - 8 * (k));                   \
+                fu_.x = keep_if(top_.x & bot_.x, F2.x);                                 \
+                fu_.y = keep_if(top_.y & bot_.y, F2.y);                                 \
                 GGS_BLEND(k, fu_);                                                      \
                 goto done;                                                              \
             }                                                                           \
-            /* scalar row limits (readfirstlane keeps them off the VALU) */             \
-            if (rowb < ufirst(y0 - 8 * (k))) fu_.x = 0.0f;  /* rows above y0 */         \
-            if (rowb < ufirst(y0 - 8 * (k) - 4)) fu_.y = 0.0f;                          \
+            fu_.x = keep_if(top_.x, F2.x);                                              \
+            fu_.y = keep_if(top_.y, F2.y);                                              \
             GGS_BLEND(k, fu_);                                                          \
             /* guard on the seed's bits (f >= 0: unsigned order = float order);  */     \
             /* dead lanes (px = -inf) excluded                                    */     \
@@ -349,9 +371,11 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 #define GGS_LAST(k)                                                                     \
     case k:                                                                             \
         if (k < NPK) {                                                                  \
-            f2_t fu_ = F2 * R2;                                                         \
-            if (rowb > ufirst(y1 - 8 * (k))) fu_.x = 0.0f;  /* rows below y1 */         \
-            if (rowb > ufirst(y1 - 8 * (k) - 4)) fu_.y = 0.0f;                          \
+            const f2_t fr_ = F2 * R2;                                                   \
+            const PairLanes bot_ = rows_upto(y1 - ty0 - 8 * (k));                       \
+            f2_t fu_;                                                                   \
+            fu_.x = keep_if(bot_.x, fr_.x);                                             \
+            fu_.y = keep_if(bot_.y, fr_.y);                                             \
             GGS_BLEND(k, fu_);                                                          \
         }                                                                               \
         break;
@@ -452,23 +476,30 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             }
         }
     } else {
-        // The target plan (plan_kernel) holds (t_r, t_g, t_b, w) per pixel in this
-        // wave's lane order, w already mode-specific and 0 outside the image:
-        // one coalesced 16-B load per pixel, no address math, no bounds tests.
-        float acc = 0.0f;
+        // The target plan (plan_kernel) holds, per lane and row-group pair
+        // (g, g+1) = (2k, 2k+1), two float4s: (t_r, t_r', t_g, t_g') and
+        // (t_b, t_b', w, w'), w already mode-specific and 0 outside the image:
+        // coalesced 16-B loads, no address math, no bounds tests, and the pair
+        // lines up with the packed accumulators (two pixels per v_pk op).
         const float4* __restrict__ P = plan + (int64_t)(t * 4 + wv) * RG * 64 + lane;
+        f2_t accp = 0.0f;
 #pragma unroll
-        for (int g = 0; g < RG; ++g) {
-            const float4 q = P[g * 64];
-            const float cr = fminf(fmaxf(__builtin_fmaf(T[g], bg_r, R[g]), 0.0f), 1.0f);
-            const float cg = fminf(fmaxf(__builtin_fmaf(T[g], bg_g, G[g]), 0.0f), 1.0f);
-            const float cb = fminf(fmaxf(__builtin_fmaf(T[g], bg_b, Bl[g]), 0.0f), 1.0f);
-            const float dr = cr - q.x;
-            const float dg = cg - q.y;
-            const float db = cb - q.z;
-            const float d2 = dr * dr + dg * dg + db * db;
-            acc += q.w * d2;
+        for (int k = 0; k < NPK; ++k) {
+            const float4 qa = P[(2 * k) * 64], qb = P[(2 * k + 1) * 64];
+            f2_t c_r, c_g, c_b;       // clamp folds into the scalar v_fma (clamp bit)
+            c_r.x = fminf(fmaxf(__builtin_fmaf(T[2 * k], bg_r, R[2 * k]), 0.0f), 1.0f);
+            c_r.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_r, R[2 * k + 1]), 0.0f), 1.0f);
+            c_g.x = fminf(fmaxf(__builtin_fmaf(T[2 * k], bg_g, G[2 * k]), 0.0f), 1.0f);
+            c_g.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_g, G[2 * k + 1]), 0.0f), 1.0f);
+            c_b.x = fminf(fmaxf(__builtin_fmaf(T[2 * k], bg_b, Bl[2 * k]), 0.0f), 1.0f);
+            c_b.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_b, Bl[2 * k + 1]), 0.0f), 1.0f);
+            const f2_t dr = c_r - (f2_t){qa.x, qa.y};
+            const f2_t dg = c_g - (f2_t){qa.z, qa.w};
+            const f2_t db = c_b - (f2_t){qb.x, qb.y};
+            const f2_t d2 = fma2(dr, dr, fma2(dg, dg, db * db));
+            accp = fma2((f2_t){qb.z, qb.w}, d2, accp);
         }
+        float acc = accp.x + accp.y;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if (lane == 0)        // one partial per (candidate, tile, strip): no block barrier
@@ -480,12 +511,14 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 // ---------------------------------------------------------------------------
 // target plan: the fitness epilogue's inputs re-laid out in raster lane order
 // ---------------------------------------------------------------------------
-// One wave per (tile, strip): plan[((t*4 + strip)*RG + g)*64 + lane] =
-// (t_r, t_g, t_b, w) of the pixel that lane owns in row group g; w is the
-// pixel weight of fitness.py:17-31 for the mode (1 / mask / 1+beta*clamp(mask))
-// and 0 outside the image.  wpartials[t*4 + strip] = the strip's sum of w
-// (per-lane in row order, then a lane butterfly).  Target and mask are constant
-// over a GA run, so the plan is built once per (target, mask, mode, beta).
+// One wave per (tile, strip).  For the row-group pair (2k, 2k+1) of the pixel
+// column this lane owns: plan[((t*4 + strip)*RG + 2k)*64 + lane] =
+// (t_r, t_r', t_g, t_g') and [... + 2k+1] = (t_b, t_b', w, w') (primed: row
+// group 2k+1), the raster epilogue's packed order; w is the pixel weight of
+// fitness.py:17-31 for the mode (1 / mask / 1+beta*clamp(mask)) and 0 outside
+// the image.  wpartials[t*4 + strip] = the strip's sum of w (per-lane in row
+// order, then a lane butterfly).  Target and mask are constant over a GA run,
+// so the plan is built once per (target, mask, mode, beta).
 __global__ void __launch_bounds__(64)
 plan_kernel(const float* __restrict__ target, const float* __restrict__ mask, int mode, float beta,
             int H, int W, int nTX, float4* __restrict__ plan, float* __restrict__ wpartials) {
@@ -495,16 +528,22 @@ plan_kernel(const float* __restrict__ target, const float* __restrict__ mask, in
     const int col = tx0 + wv * 16 + (lane & 15), ph = lane >> 4;
     float4* __restrict__ P = plan + (int64_t)blockIdx.x * RG * 64 + lane;
     float wacc = 0.0f;
-    for (int g = 0; g < RG; ++g) {
-        const int row = ty0 + 4 * g + ph;
-        const bool ok = (row < H) & (col < W);
-        const int64_t p = (int64_t)min(row, H - 1) * W + min(col, W - 1);
-        float wgt = 1.0f;
-        if (mode == GGS_FIT_WEIGHTED) wgt = mask[p];
-        if (mode == GGS_FIT_BOOST) wgt = 1.0f + beta * fminf(fmaxf(mask[p], 0.0f), 1.0f);
-        wgt = ok ? wgt : 0.0f;
-        P[g * 64] = make_float4(target[p * 3 + 0], target[p * 3 + 1], target[p * 3 + 2], wgt);
-        wacc += wgt;
+    for (int k = 0; k < RG / 2; ++k) {
+        float tr[2], tg[2], tb[2], wg[2];
+        for (int h = 0; h < 2; ++h) {
+            const int row = ty0 + 4 * (2 * k + h) + ph;
+            const bool ok = (row < H) & (col < W);
+            const int64_t p = (int64_t)min(row, H - 1) * W + min(col, W - 1);
+            float wgt = 1.0f;
+            if (mode == GGS_FIT_WEIGHTED) wgt = mask[p];
+            if (mode == GGS_FIT_BOOST) wgt = 1.0f + beta * fminf(fmaxf(mask[p], 0.0f), 1.0f);
+            wgt = ok ? wgt : 0.0f;
+            tr[h] = target[p * 3 + 0]; tg[h] = target[p * 3 + 1]; tb[h] = target[p * 3 + 2];
+            wg[h] = wgt;
+            wacc += wgt;
+        }
+        P[(2 * k) * 64] = make_float4(tr[0], tr[1], tg[0], tg[1]);
+        P[(2 * k + 1) * 64] = make_float4(tb[0], tb[1], wg[0], wg[1]);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wacc += __shfl_xor(wacc, o);
