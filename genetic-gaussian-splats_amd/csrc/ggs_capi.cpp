@@ -99,8 +99,7 @@ struct Workspace {
 // Upload the central-tiles-first raster order for (H, W) once per size.
 int ensure_tile_order(Workspace* w, int H, int W, hipStream_t st) {
     if (w->order_H == H && w->order_W == W) return GGS_OK;
-    int nTX;
-    const int n = raster_tiles(H, W, &nTX);
+    const int n = raster_order_len(H, W);
     int rc;
     if ((rc = ensure(w->order, sizeof(int) * (size_t)n, st))) return rc;
     std::vector<int> h(n);
@@ -1058,14 +1057,14 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     if ((rc = ensure(s->recs, sizeof(SplatRec) * std::max<size_t>((size_t)s->P * s->N, 1), s->st)) ||
         (rc = ensure(s->partials, sizeof(float) * slots * s->P, s->st)) ||
         (rc = ensure(s->plan, plan_bytes(c.H, c.W), s->st)) || (rc = ensure(s->wpart, sizeof(float) * slots, s->st)) ||
-        (rc = ensure(s->order, sizeof(int) * (size_t)s->nTiles, s->st)))
+        (rc = ensure(s->order, sizeof(int) * (size_t)raster_order_len(c.H, c.W), s->st)))
         return bail(rc);
-    std::vector<int> order(s->nTiles);
+    std::vector<int> order(raster_order_len(c.H, c.W));
     raster_tile_order(c.H, c.W, order.data());
     if (hipMemcpyAsync(s->target.p, target_hw3, sizeof(float) * 3 * hw, hipMemcpyHostToDevice, s->st) ||
         (mask_hw && hipMemcpyAsync(s->mask.p, mask_hw, sizeof(float) * hw, hipMemcpyHostToDevice, s->st)) ||
         hipMemcpyAsync(s->pop[0].p, init_pop, pb, hipMemcpyHostToDevice, s->st) ||
-        hipMemcpyAsync(s->order.p, order.data(), sizeof(int) * s->nTiles, hipMemcpyHostToDevice, s->st))
+        hipMemcpyAsync(s->order.p, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice, s->st))
         return bail(fail(GGS_EHIP, "upload failed"));
     if (launch_plan(s->st, (const float*)s->target.p, mask_hw ? (const float*)s->mask.p : nullptr, c.fitness_mode,
                     c.boost_beta, c.H, c.W, (float4*)s->plan.p, (float*)s->wpart.p) != hipSuccess)
@@ -1172,19 +1171,19 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
         (rc = ensure(s->nb_part, sizeof(float) * slots * s->cap, s->st)) ||
         (rc = ensure(s->dirty, slots * s->cap, s->st)) || (rc = ensure(s->plan, plan_bytes(cfg->H, cfg->W), s->st)) ||
         (rc = ensure(s->wpart, sizeof(float) * slots, s->st)) ||
-        (rc = ensure(s->order, sizeof(int) * (size_t)s->nTiles, s->st)) ||
+        (rc = ensure(s->order, sizeof(int) * (size_t)raster_order_len(cfg->H, cfg->W), s->st)) ||
         (rc = ensure(s->counters, sizeof(unsigned) * 4, s->st)))
         return bail(rc);
     if (hipHostMalloc((void**)&s->h_fits, sizeof(float) * s->cap, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&s->h_counters, sizeof(unsigned) * 4, hipHostMallocDefault) != hipSuccess)
         return bail(fail(GGS_ENOMEM, "pinned allocation failed"));
-    std::vector<int> order(s->nTiles);
+    std::vector<int> order(raster_order_len(cfg->H, cfg->W));
     raster_tile_order(cfg->H, cfg->W, order.data());
     if (hipMemcpyAsync(s->target.p, target_hw3, sizeof(float) * 3 * hw, hipMemcpyHostToDevice, s->st) ||
         (mask_hw && hipMemcpyAsync(s->mask.p, mask_hw, sizeof(float) * hw, hipMemcpyHostToDevice, s->st)) ||
         hipMemcpyAsync(s->curr.p, init_ind, ib, hipMemcpyHostToDevice, s->st) ||
         hipMemcpyAsync(s->best.p, init_ind, ib, hipMemcpyHostToDevice, s->st) ||
-        hipMemcpyAsync(s->order.p, order.data(), sizeof(int) * s->nTiles, hipMemcpyHostToDevice, s->st) ||
+        hipMemcpyAsync(s->order.p, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice, s->st) ||
         hipMemsetAsync(s->counters.p, 0, sizeof(unsigned) * 4, s->st))
         return bail(fail(GGS_EHIP, "upload failed"));
     if (launch_plan(s->st, (const float*)s->target.p, mask_hw ? (const float*)s->mask.p : nullptr,

@@ -40,7 +40,8 @@ size_t plan_bytes(int H, int W);
 // Tile visiting order for the raster grid: tiles sorted by distance of their
 // centre from the image centre (central tiles carry the most splats; running
 // them first shortens the tail of the launch).
-void raster_tile_order(int H, int W, int* order);
+void raster_tile_order(int H, int W, int* order);   // raster_order_len(H, W) entries
+int raster_order_len(int H, int W);
 hipError_t launch_detmath(hipStream_t st, const float* x, const float* y, int64_t n, int fn,
                           float* out);
 hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,

@@ -219,10 +219,12 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 
     const int lane = threadIdx.x & 63;
     const int wib = ufirst((int)(threadIdx.x >> 6));  // wave in block (uniform: keeps control on SALU)
-    const int blk = blockIdx.x / SPB;
-    const int wv = (blockIdx.x % SPB) * WPB + wib;    // strip 0..3 of the tile
-    const int b = blk % B;            // tile-major grid: consecutive blocks share a tile
-    const int t = tile_order ? tile_order[blk / B] : blk / B;   // heavy (central) tiles first
+    // strip-major grid: B consecutive blocks run one strip (group) for every
+    // candidate; groups go central (heavy) first to shorten the grid's tail
+    const int grp = tile_order ? tile_order[blockIdx.x / B] : (int)(blockIdx.x / B);
+    const int b = blockIdx.x % B;
+    const int t = grp / SPB;
+    const int wv = (grp % SPB) * WPB + wib;           // strip 0..3 of the tile
     const int tx0 = (t % nTX) * TILE;
     const int ty0 = (t / nTX) * TILE_H;
     const int ty1 = min(ty0 + TILE_H, H) - 1;
@@ -663,18 +665,26 @@ hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_
     return hipGetLastError();
 }
 
+// Dispatch order of the (tile, block-in-tile) groups: nearest the canvas
+// centre first.  Splat density, and so a strip's cull list, peaks in the middle
+// (AABBs are clipped at the borders); running the long strips first leaves the
+// short ones to fill the grid's last round (list-scheduling model of the bench
+// population: 1.135x -> 1.098x the ideal makespan; tile-granular order 1.135x).
 void raster_tile_order(int H, int W, int* order) {
     int nTX;
-    const int n = raster_tiles(H, W, &nTX);
+    const int n = raster_tiles(H, W, &nTX) * SPB;
     std::vector<std::pair<double, int>> d(n);
-    for (int t = 0; t < n; ++t) {
-        const double cx = (t % nTX) * TILE + 0.5 * TILE - 0.5 * W;
+    for (int g = 0; g < n; ++g) {
+        const int t = g / SPB, s = g % SPB;
+        const double cx = (t % nTX) * TILE + (s + 0.5) * (TILE / SPB) - 0.5 * W;
         const double cy = (t / nTX) * TILE_H + 0.5 * TILE_H - 0.5 * H;
-        d[t] = {cx * cx + cy * cy, t};
+        d[g] = {cx * cx + cy * cy, g};
     }
     std::stable_sort(d.begin(), d.end());
-    for (int t = 0; t < n; ++t) order[t] = d[t].second;
+    for (int g = 0; g < n; ++g) order[g] = d[g].second;
 }
+
+int raster_order_len(int H, int W) { return raster_tiles(H, W, nullptr) * SPB; }
 
 int raster_tiles(int H, int W, int* nTX) {
     const int tx = (W + TILE - 1) / TILE, ty = (H + TILE_H - 1) / TILE_H;
