@@ -353,40 +353,40 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             // block (the walk's scalar branches split blocks), so the scheduler
             // overlaps one pair's blend with the next pair's recurrence
             // (4 per block measured slower: tools/ablate.py 0.245 vs 0.251 ms).
+            // The last pair (rows below y1 masked) is inlined at both exits of
+            // each step, so leaving the walk costs no second switch.
+#define GGS_LASTB(k)                                                                    \
+    if ((k) < NPK) {                                                                    \
+        const f2_t fr_ = F2 * R2;                                                       \
+        const PairLanes bot_ = rows_upto(y1 - ty0 - 8 * (k));                           \
+        f2_t fu_;                                                                       \
+        fu_.x = keep_if(bot_.x, fr_.x);                                                 \
+        fu_.y = keep_if(bot_.y, fr_.y);                                                 \
+        GGS_BLEND(k, fu_);                                                              \
+    }
 #define GGS_MID2(k, k1, k2)                                                             \
     u##k:                                                                               \
         if (kB > (k2)) {                                                                \
             GGS_BLEND_REC(k1) GGS_BLEND_REC(k2)                                         \
             goto u##k2;                                                                 \
         }                                                                               \
-        if (kB == (k2)) { GGS_BLEND_REC(k1) }                                           \
-        goto last;
+        if (kB == (k2)) {                                                               \
+            GGS_BLEND_REC(k1)                                                           \
+            GGS_LASTB(k2)                                                               \
+            goto done;                                                                  \
+        }                                                                               \
+        GGS_LASTB(k1)                                                                   \
+        goto done;
             GGS_MID2(0, 1, 2) GGS_MID2(1, 2, 3) GGS_MID2(2, 3, 4) GGS_MID2(3, 4, 5)
             GGS_MID2(4, 5, 6) GGS_MID2(5, 6, 7) GGS_MID2(6, 7, 8) GGS_MID2(7, 8, 9)
             GGS_MID2(8, 9, 10) GGS_MID2(9, 10, 11) GGS_MID2(10, 11, 12) GGS_MID2(11, 12, 13)
             GGS_MID2(12, 13, 14) GGS_MID2(13, 14, 15)
 #undef GGS_MID2
-        u14:
+        u14:                          // pair 15 is the last one there is
+            GGS_LASTB(15)
+            goto done;
+#undef GGS_LASTB
         u15:
-        last:
-            switch (kB) {
-#define GGS_LAST(k)                                                                     \
-    case k:                                                                             \
-        if (k < NPK) {                                                                  \
-            const f2_t fr_ = F2 * R2;                                                   \
-            const PairLanes bot_ = rows_upto(y1 - ty0 - 8 * (k));                       \
-            f2_t fu_;                                                                   \
-            fu_.x = keep_if(bot_.x, fr_.x);                                             \
-            fu_.y = keep_if(bot_.y, fr_.y);                                             \
-            GGS_BLEND(k, fu_);                                                          \
-        }                                                                               \
-        break;
-                GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
-                GGS_LAST(7) GGS_LAST(8) GGS_LAST(9) GGS_LAST(10) GGS_LAST(11) GGS_LAST(12)
-                GGS_LAST(13) GGS_LAST(14) GGS_LAST(15)
-#undef GGS_LAST
-                default: __builtin_unreachable();
-            }
             goto done;
             // exact walk (guard tripped): the exponent per pair as before
 #define GGS_XMID(kp, k) x##kp: if (kB == k) goto xlast; if (k < NPK) GGS_PK(k, false);
