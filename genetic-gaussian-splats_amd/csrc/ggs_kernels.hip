@@ -308,6 +308,34 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             // A seed below 2^-100 (0x0D800000) on a live lane (tiny corner of a thin rotated
             // splat) would lose the recurrence's precision: that wave walks this
             // splat with the exact exponent instead (wave-uniform, ~0.3 % of walks).
+            // Full-height visits (the splat spans the strip's 128 rows: ~45 % of
+            // them on the bench population) need no row mask and no walk exit
+            // test: one straight-line block, the same arithmetic as the general
+            // walk (kA = 0, kB = NPK-1, all-ones masks), so the same bits.
+            if (y0 <= ty0 && y1 >= ty0 + TILE_H - 1) {
+                const f2_t e_ = fma2(qyv, fma2(Cc2, qyv, bx2), px2);
+                F2.x = GGS_EXP2(e_.x);
+                F2.y = GGS_EXP2(e_.y);
+                GGS_BLEND(0, F2);
+                if (__ballot((px > -__builtin_inff()) &
+                             (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u)))
+                    goto x0;
+                const float t8_ = px > -__builtin_inff() ? __builtin_fmaf(bx, 8.0f, s.c64)
+                                                         : -__builtin_inff();
+                const f2_t d_ = fma2(qyv, (f2_t)s.c16, (f2_t)t8_);
+                R2.x = GGS_EXP2(d_.x);
+                R2.y = GGS_EXP2(d_.y);
+#define GGS_FULL(k)                                                                     \
+    if ((k) >= 1 && (k) < NPK - 1) {                                                    \
+        GGS_BLEND_REC(k)                                                                \
+    } else if ((k) == NPK - 1) {      /* last pair: no ratio update */                  \
+        F2 = F2 * R2;                                                                   \
+        GGS_BLEND(k, F2);                                                               \
+    }
+                GGS_FOR16P(GGS_FULL)
+#undef GGS_FULL
+                goto done;
+            }
             switch (kA) {
 #define GGS_FIRST(k)                                                                    \
     case k:                                                                             \
