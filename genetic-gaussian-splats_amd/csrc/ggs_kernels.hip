@@ -269,7 +269,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         bbn = *reinterpret_cast<const int4*>(&crec[max(i - 64, 0)].x0);
         const bool hit = (i >= 0) & (bb.w >= ty0) & (bb.z <= ty1) & (bb.y >= sx0) & (bb.x <= sx0 + 15);
         const uint64_t m = __ballot(hit);
-        if (hit) list[cnt + __popcll(m & lt_mask)] = i;
+        if (hit) list[cnt + __popcll(m & lt_mask)] = i * (int)sizeof(SplatRec);   // byte offset
         cnt += __popcll(m);
         if (cnt <= CAP - 64 && base + 64 < N) continue;
         if (cnt == 0) continue;
@@ -279,13 +279,20 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         //     record is fetched while the current one is blended; list indices
         //     are read 64 at a time into a VGPR (one per lane) and picked with
         //     v_readlane, so no LDS latency sits on the per-splat path ---------
-        int idxv = list[min(lane, cnt - 1)];
-        SplatRec nxt = crec[__builtin_amdgcn_readlane(idxv, 0)];
+        // (byte offsets: the record load takes the readlane result as its
+        //  32-bit SGPR offset; past the list end it reloads a listed record)
+        const char* __restrict__ cbase = reinterpret_cast<const char*>(crec);
+        int offv = list[min(lane, cnt - 1)];
+        SplatRec nxt = *reinterpret_cast<const SplatRec*>(cbase + (unsigned)__builtin_amdgcn_readlane(offv, 0));
+        int jr = 63;                  // last j before the next 64 offsets are needed
         for (int j = 0; j < cnt; ++j) {
             const SplatRec s = nxt;
-            const int jn = min(j + 1, cnt - 1);
-            if ((jn & 63) == 0 && jn != j) idxv = list[min(jn + lane, cnt - 1)];
-            nxt = crec[__builtin_amdgcn_readlane(idxv, jn & 63)];   // waited at the latch
+            if (j == jr) {
+                jr += 64;
+                offv = list[min(j + 1 + lane, cnt - 1)];
+            }
+            nxt = *reinterpret_cast<const SplatRec*>(
+                cbase + (unsigned)__builtin_amdgcn_readlane(offv, (j + 1) & 63));   // waited at the latch
             const int x0 = s.x0, x1 = s.x1, y0 = s.y0, y1 = s.y1;
             const int gA = max(y0 - ty0, 0) >> 2;             // first / last row group
             const int gB = min(y1 - ty0, TILE_H - 1) >> 2;
