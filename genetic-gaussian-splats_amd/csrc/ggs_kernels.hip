@@ -92,6 +92,9 @@ constexpr int WPB = GGS_WPB;      // waves per workgroup (each wave owns one 16-
 constexpr int NT = 64 * WPB;      // threads per workgroup
 constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
+#ifndef GGS_PREFETCH
+#define GGS_PREFETCH 1            // next splat record loaded while the current one is blended
+#endif
 #ifndef GGS_OCC
 #define GGS_OCC 3                 // waves per SIMD the register budget is sized for (158 VGPRs)
 #endif
@@ -283,6 +286,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         //  32-bit SGPR offset; past the list end it reloads a listed record)
         const char* __restrict__ cbase = reinterpret_cast<const char*>(crec);
         int offv = list[min(lane, cnt - 1)];
+#if GGS_PREFETCH
         SplatRec nxt = *reinterpret_cast<const SplatRec*>(cbase + (unsigned)__builtin_amdgcn_readlane(offv, 0));
         int jr = 63;                  // last j before the next 64 offsets are needed
         for (int j = 0; j < cnt; ++j) {
@@ -293,6 +297,12 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             }
             nxt = *reinterpret_cast<const SplatRec*>(
                 cbase + (unsigned)__builtin_amdgcn_readlane(offv, (j + 1) & 63));   // waited at the latch
+#else
+        for (int j = 0; j < cnt; ++j) {
+            if (j > 0 && (j & 63) == 0) offv = list[min(j + lane, cnt - 1)];
+            const SplatRec s = *reinterpret_cast<const SplatRec*>(
+                cbase + (unsigned)__builtin_amdgcn_readlane(offv, j & 63));
+#endif
             const int x0 = s.x0, x1 = s.x1, y0 = s.y0, y1 = s.y1;
             const int gA = max(y0 - ty0, 0) >> 2;             // first / last row group
             const int gB = min(y1 - ty0, TILE_H - 1) >> 2;
