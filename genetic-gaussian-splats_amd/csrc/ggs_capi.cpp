@@ -96,7 +96,7 @@ struct Workspace {
     uint64_t plan_key = 0;            // inputs the plan was built from (0: none / volatile)
 };
 
-// Upload the central-tiles-first raster order for (H, W) once per size.
+// Upload the centre-first raster dispatch order for (H, W) once per size.
 int ensure_tile_order(Workspace* w, int H, int W, hipStream_t st) {
     if (w->order_H == H && w->order_W == W) return GGS_OK;
     const int n = raster_order_len(H, W);
