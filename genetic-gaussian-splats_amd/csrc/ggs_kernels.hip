@@ -93,7 +93,7 @@ constexpr int NT = 64 * WPB;      // threads per workgroup
 constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
 #ifndef GGS_PREFETCH
-#define GGS_PREFETCH 1            // next splat record loaded while the current one is blended
+#define GGS_PREFETCH 2            // next record loaded while the current one is blended (2: two alternating register sets)
 #endif
 #ifndef GGS_OCC
 #define GGS_OCC 3                 // waves per SIMD the register budget is sized for (158 VGPRs)
@@ -286,23 +286,8 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         //  32-bit SGPR offset; past the list end it reloads a listed record)
         const char* __restrict__ cbase = reinterpret_cast<const char*>(crec);
         int offv = list[min(lane, cnt - 1)];
-#if GGS_PREFETCH
-        SplatRec nxt = *reinterpret_cast<const SplatRec*>(cbase + (unsigned)__builtin_amdgcn_readlane(offv, 0));
-        int jr = 63;                  // last j before the next 64 offsets are needed
-        for (int j = 0; j < cnt; ++j) {
-            const SplatRec s = nxt;
-            if (j == jr) {
-                jr += 64;
-                offv = list[min(j + 1 + lane, cnt - 1)];
-            }
-            nxt = *reinterpret_cast<const SplatRec*>(
-                cbase + (unsigned)__builtin_amdgcn_readlane(offv, (j + 1) & 63));   // waited at the latch
-#else
-        for (int j = 0; j < cnt; ++j) {
-            if (j > 0 && (j & 63) == 0) offv = list[min(j + lane, cnt - 1)];
-            const SplatRec s = *reinterpret_cast<const SplatRec*>(
-                cbase + (unsigned)__builtin_amdgcn_readlane(offv, j & 63));
-#endif
+        // one (splat, strip) visit: cull-list record s -> the strip's accumulators
+        auto visit = [&](const SplatRec& s) __attribute__((always_inline)) {
             const int x0 = s.x0, x1 = s.x1, y0 = s.y0, y1 = s.y1;
             const int gA = max(y0 - ty0, 0) >> 2;             // first / last row group
             const int gB = min(y1 - ty0, TILE_H - 1) >> 2;
@@ -486,7 +471,45 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             asm volatile("" :: "v"(px), "v"(bx), "v"(qy0), "v"(rlo), "s"(rspan), "s"(Cc), "s"(cr),
                          "s"(cg), "s"(cb), "s"(gA), "s"(gB));
 #endif
+        };
+#if GGS_PREFETCH == 2
+        // two records in alternating SGPR sets: the next record is loaded into
+        // the set the finished visit used, so no register rotation at the latch
+        auto load_at = [&](int jj) __attribute__((always_inline)) {
+            return *reinterpret_cast<const SplatRec*>(
+                cbase + (unsigned)__builtin_amdgcn_readlane(offv, jj & 63));
+        };
+        SplatRec ra = load_at(0);
+        int jr = 63;                  // last j before the next 64 offsets are needed
+        for (int j = 0;;) {
+            if (j == jr) { jr += 64; offv = list[min(j + 1 + lane, cnt - 1)]; }
+            const SplatRec rb = load_at(j + 1);
+            visit(ra);
+            if (++j >= cnt) break;
+            if (j == jr) { jr += 64; offv = list[min(j + 1 + lane, cnt - 1)]; }
+            ra = load_at(j + 1);
+            visit(rb);
+            if (++j >= cnt) break;
         }
+#elif GGS_PREFETCH
+        SplatRec nxt = *reinterpret_cast<const SplatRec*>(cbase + (unsigned)__builtin_amdgcn_readlane(offv, 0));
+        int jr = 63;                  // last j before the next 64 offsets are needed
+        for (int j = 0; j < cnt; ++j) {
+            const SplatRec s = nxt;
+            if (j == jr) {
+                jr += 64;
+                offv = list[min(j + 1 + lane, cnt - 1)];
+            }
+            nxt = *reinterpret_cast<const SplatRec*>(
+                cbase + (unsigned)__builtin_amdgcn_readlane(offv, (j + 1) & 63));   // waited at the latch
+            visit(s);
+        }
+#else
+        for (int j = 0; j < cnt; ++j) {
+            if (j > 0 && (j & 63) == 0) offv = list[min(j + lane, cnt - 1)];
+            visit(*reinterpret_cast<const SplatRec*>(cbase + (unsigned)__builtin_amdgcn_readlane(offv, j & 63)));
+        }
+#endif
         cnt = 0;
     }
 
