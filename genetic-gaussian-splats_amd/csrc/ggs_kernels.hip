@@ -131,7 +131,8 @@ __device__ __forceinline__ float keep_if(uint64_t lanes, float f) {
 // MASKED adds the per-lane row test for the AABB's first/last row block.
 // Performance-ablation switch (tools/ablate.py; 0 in every shipped build):
 // 1 = exp replaced by a multiply, 2 = no row-group bodies, 3 = red channel only,
-// 4 = cull + epilogue only (no per-splat work), 5 = no epilogue, 6 = dispatch only.
+// 4 = cull + epilogue only (no per-splat work), 5 = no epilogue, 6 = dispatch only,
+// 7 = every wave reads one of 8 candidates' records (record-cache locality probe).
 #ifndef GGS_ABL
 #define GGS_ABL 0
 #endif
@@ -256,7 +257,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 #endif
 #undef GGS_DECL
 
-    const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
+    const SplatRec* __restrict__ crec = recs + (GGS_ABL == 7 ? (int64_t)(b & 7) : (int64_t)b) * N;   // ABL 7: 8 shared candidates
     int* __restrict__ list = &lists[0][0] + wib * CAP;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
@@ -289,8 +290,9 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         // one (splat, strip) visit: cull-list record s -> the strip's accumulators
         auto visit = [&](const SplatRec& s) __attribute__((always_inline)) {
             const int x0 = s.x0, x1 = s.x1, y0 = s.y0, y1 = s.y1;
-            const int gA = max(y0 - ty0, 0) >> 2;             // first / last row group
-            const int gB = min(y1 - ty0, TILE_H - 1) >> 2;
+            const int dy0 = y0 - ty0, dy1 = y1 - ty0;          // AABB rows relative to the tile
+            const int gA = max(dy0, 0) >> 2;                   // first / last row group
+            const int gB = min(dy1, TILE_H - 1) >> 2;
             const float Cc = s.Cc, cr = s.r, cg = s.g, cb = s.b;
             const float qx = Xf - s.cx;
             const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
@@ -314,14 +316,16 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             // them on the bench population) need no row mask and no walk exit
             // test: one straight-line block, the same arithmetic as the general
             // walk (kA = 0, kB = NPK-1, all-ones masks), so the same bits.
-            if (y0 <= ty0 && y1 >= ty0 + TILE_H - 1) {
+            if (max(dy0, TILE_H - 1 - dy1) <= 0) {            // y0 <= ty0 and y1 >= ty0 + 127
                 const f2_t e_ = fma2(qyv, fma2(Cc2, qyv, bx2), px2);
                 F2.x = GGS_EXP2(e_.x);
                 F2.y = GGS_EXP2(e_.y);
-                GGS_BLEND(0, F2);
                 if (__ballot((px > -__builtin_inff()) &
-                             (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u)))
+                             (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u))) {
+                    GGS_BLEND(0, F2);
                     goto x0;
+                }
+                GGS_BLEND(0, F2);
                 const float t8_ = px > -__builtin_inff() ? __builtin_fmaf(bx, 8.0f, s.c64)
                                                          : -__builtin_inff();
                 const f2_t d_ = fma2(qyv, (f2_t)s.c16, (f2_t)t8_);
