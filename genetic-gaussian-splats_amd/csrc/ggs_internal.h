@@ -16,7 +16,7 @@ struct __attribute__((aligned(16))) SplatRec {
     float cx, cy, A, Bc;
     float Cc, la, r, g;
     float b;
-    float rho, c16, c64;   // row-recurrence constants: 2^(128 Cc), 16 Cc, 64 Cc (8-row step)
+    float rho, c16, rho4;  // row-recurrence constants: 2^(128 Cc), 16 Cc, 2^(64 Cc) (8-row step)
     int x0, x1, y0, y1;
 };
 static_assert(sizeof(SplatRec) == 64, "SplatRec must be 64 bytes");

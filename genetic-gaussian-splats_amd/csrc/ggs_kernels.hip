@@ -326,11 +326,10 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
                     goto x0;
                 }
                 GGS_BLEND(0, F2);
-                const float t8_ = px > -__builtin_inff() ? __builtin_fmaf(bx, 8.0f, s.c64)
-                                                         : -__builtin_inff();
-                const f2_t d_ = fma2(qyv, (f2_t)s.c16, (f2_t)t8_);
-                R2.x = GGS_EXP2(d_.x);
-                R2.y = GGS_EXP2(d_.y);
+                // d(qy) = 16 Cc (qy + 4) + 8 bx; the .y row's ratio is 2^(64 Cc) times it
+                const float t8_ = px > -__builtin_inff() ? 8.0f * bx : -__builtin_inff();
+                R2.x = GGS_EXP2(__builtin_fmaf(qyv.y, s.c16, t8_));
+                R2.y = R2.x * s.rho4;
 #define GGS_FULL(k)                                                                     \
     if ((k) >= 1 && (k) < NPK - 1) {                                                    \
         GGS_BLEND_REC(k)                                                                \
@@ -367,12 +366,11 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             if (__ballot((px > -__builtin_inff()) &                                     \
                          (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u))) \
                 goto x##k;                                                              \
-            /* live lanes: d <= -e(seed) <= 100; dead lanes: d = -inf -> r = 0   */     \
-            const float t8_ = px > -__builtin_inff() ? __builtin_fmaf(bx, 8.0f, s.c64)  \
-                                                     : -__builtin_inff();               \
-            const f2_t d_ = fma2(qy_, (f2_t)s.c16, (f2_t)t8_);                          \
-            R2.x = GGS_EXP2(d_.x);                                                      \
-            R2.y = GGS_EXP2(d_.y);                                                      \
+            /* live lanes: d <= -e(seed) <= 100; dead lanes: d = -inf -> r = 0;  */     \
+            /* d(qy) = 16 Cc (qy + 4) + 8 bx, the .y row's ratio 2^(64 Cc) times */     \
+            const float t8_ = px > -__builtin_inff() ? 8.0f * bx : -__builtin_inff();  \
+            R2.x = GGS_EXP2(__builtin_fmaf(qy_.y, s.c16, t8_));                         \
+            R2.y = R2.x * s.rho4;                                                       \
             goto u##k;                                                                  \
         }                                                                               \
         break;

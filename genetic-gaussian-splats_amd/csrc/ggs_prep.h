@@ -87,11 +87,12 @@ __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
     r.r = p.rc;
     r.g = p.gc;
     r.b = p.bc;
-    // f(qy + 8) = f(qy) * 2^d(qy),  d(qy) = e(qy + 8) - e(qy) = 16 Cc qy + 64 Cc + 8 bx,
-    // d(qy + 8) = d(qy) + 128 Cc  ->  the raster walks rows with two multiplies.
+    // f(qy + 8) = f(qy) * 2^d(qy),  d(qy) = e(qy + 8) - e(qy) = 16 Cc (qy + 4) + 8 bx,
+    // d(qy + 8) = d(qy) + 128 Cc  ->  the raster walks rows with two multiplies;
+    // d(qy + 4) = d(qy) + 64 Cc   ->  the pair's second row ratio is one multiply.
     r.rho = __builtin_amdgcn_exp2f(128.0f * r.Cc);
     r.c16 = 16.0f * r.Cc;
-    r.c64 = 64.0f * r.Cc;
+    r.rho4 = __builtin_amdgcn_exp2f(64.0f * r.Cc);
     r.x0 = p.x0;
     r.x1 = p.x1;
     r.y0 = p.y0;
