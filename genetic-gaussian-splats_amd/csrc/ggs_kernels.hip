@@ -92,6 +92,9 @@ constexpr int WPB = GGS_WPB;      // waves per workgroup (each wave owns one 16-
 constexpr int NT = 64 * WPB;      // threads per workgroup
 constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
+#ifndef GGS_CULL_PF
+#define GGS_CULL_PF 1             // cull bounds loads in flight (chunks of 64 splats)
+#endif
 #ifndef GGS_PREFETCH
 #define GGS_PREFETCH 2            // next record loaded while the current one is blended (2: two alternating register sets)
 #endif
@@ -262,15 +265,29 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
 
-    // bounds of the next 64 splats are loaded one chunk ahead (latency overlap)
-    int4 bbn = *reinterpret_cast<const int4*>(&crec[max(N - 1 - lane, 0)].x0);
+    // bounds of the next 64 splats are loaded GGS_CULL_PF chunks ahead (the
+    // cull does little work per chunk, so it waits on these loads)
+    auto bounds = [&](int i) { return *reinterpret_cast<const int4*>(&crec[max(i, 0)].x0); };
+    int4 bbn = bounds(N - 1 - lane);
+#if GGS_CULL_PF >= 2
+    int4 bbn2 = bounds(N - 1 - 64 - lane);
+#endif
+#if GGS_CULL_PF >= 4
+    int4 bbn3 = bounds(N - 1 - 128 - lane), bbn4 = bounds(N - 1 - 192 - lane);
+#endif
     for (int base = 0; base < N; base += 64) {
         // --- cull 64 splats (descending index = front-to-back) against the strip:
         // one 16-B load per lane (clamped index, no short-circuit: a branchy test
         // splits it into two dependent loads), then a branch-free overlap test
         const int i = N - 1 - (base + lane);
         const int4 bb = bbn;                                                  // x0 x1 y0 y1
-        bbn = *reinterpret_cast<const int4*>(&crec[max(i - 64, 0)].x0);
+#if GGS_CULL_PF >= 4
+        bbn = bbn2; bbn2 = bbn3; bbn3 = bbn4; bbn4 = bounds(i - 256);
+#elif GGS_CULL_PF >= 2
+        bbn = bbn2; bbn2 = bounds(i - 128);
+#else
+        bbn = bounds(i - 64);
+#endif
         const bool hit = (i >= 0) & (bb.w >= ty0) & (bb.z <= ty1) & (bb.y >= sx0) & (bb.x <= sx0 + 15);
         const uint64_t m = __ballot(hit);
         if (hit) list[cnt + __popcll(m & lt_mask)] = i * (int)sizeof(SplatRec);   // byte offset
