@@ -92,6 +92,9 @@ constexpr int WPB = GGS_WPB;      // waves per workgroup (each wave owns one 16-
 constexpr int NT = 64 * WPB;      // threads per workgroup
 constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
+#ifndef GGS_XCD_SPREAD
+#define GGS_XCD_SPREAD 1          // spread each candidate's strips over the XCDs
+#endif
 #ifndef GGS_CULL_PF
 #define GGS_CULL_PF 1             // cull bounds loads in flight (chunks of 64 splats)
 #endif
@@ -103,6 +106,19 @@ constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull
 #endif
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+#ifndef GGS_TIMING
+#define GGS_TIMING 0              // diagnostic build: per-wave phase clocks (tools/probe/wave_timing.py)
+#endif
+#if GGS_TIMING
+constexpr int GGS_TIMING_WAVES = 1 << 16;
+// per wave (blockIdx, WPB = 1): realtime start, realtime end (100 MHz), cull,
+// visit and epilogue shader clocks, HW_ID | XCC_ID << 24, visits, unused
+__device__ unsigned long long g_ggs_timing[8 * GGS_TIMING_WAVES];
+#define GGS_TMARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define GGS_TMARK(v)
+#endif
 
 // Row limits as wave lane masks.  Lane l owns row phase ph = l >> 4, so "the
 // lane's row in this pair is >= / <= a wave-uniform bound" is a contiguous range
@@ -225,11 +241,24 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     }
 
     const int lane = threadIdx.x & 63;
+#if GGS_TIMING
+    const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_cull = 0, t_vis = 0, t_mark = __builtin_amdgcn_s_memtime();
+    unsigned n_vis = 0;
+#endif
     const int wib = ufirst((int)(threadIdx.x >> 6));  // wave in block (uniform: keeps control on SALU)
     // strip-major grid: B consecutive blocks run one strip (group) for every
     // candidate; groups go central (heavy) first to shorten the grid's tail
-    const int grp = tile_order ? tile_order[blockIdx.x / B] : (int)(blockIdx.x / B);
+    const int gi = blockIdx.x / B;
+    const int grp = tile_order ? tile_order[gi] : gi;
+#if GGS_XCD_SPREAD
+    // candidates rotate by one per group: with B % 8 == 0 a fixed b would stay on
+    // one XCD (blocks go round-robin to the 8 XCDs) and per-XCD work would be the
+    // sum of 16 candidates' costs (tools/probe/wave_timing.py: XCD end times 197-207 us)
+    const int b = (int)((blockIdx.x + gi) % B);
+#else
     const int b = blockIdx.x % B;
+#endif
     const int t = grp / SPB;
     const int wv = (grp % SPB) * WPB + wib;           // strip 0..3 of the tile
     const int tx0 = (t % nTX) * TILE;
@@ -295,6 +324,9 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         if (cnt <= CAP - 64 && base + 64 < N) continue;
         if (cnt == 0) continue;
         if (GGS_ABL == 4) { asm volatile("" :: "v"(list[lane])); cnt = 0; continue; }
+#if GGS_TIMING
+        { GGS_TMARK(now); t_cull += now - t_mark; t_mark = now; n_vis += cnt; }
+#endif
 
         // --- blend the list: splat params arrive in SGPRs (s_load), the next
         //     record is fetched while the current one is blended; list indices
@@ -530,6 +562,9 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         }
 #endif
         cnt = 0;
+#if GGS_TIMING
+        { GGS_TMARK(now); t_vis += now - t_mark; t_mark = now; }
+#endif
     }
 
     // --- epilogue ---------------------------------------------------------------
@@ -594,6 +629,19 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         if (lane == 0)        // one partial per (candidate, tile, strip): no block barrier
             partials[((int64_t)b * nTiles + t) * 4 + wv] = acc;
     }
+#if GGS_TIMING
+    {
+        GGS_TMARK(now);
+        const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0 && blockIdx.x < GGS_TIMING_WAVES) {
+            unsigned long long* o = g_ggs_timing + 8 * (size_t)blockIdx.x;
+            o[0] = rt_start; o[1] = rt_end; o[2] = t_cull; o[3] = t_vis; o[4] = now - t_mark;
+            o[5] = (unsigned long long)__builtin_amdgcn_s_getreg(0xF804) |
+                   ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);
+            o[6] = n_vis; o[7] = 0;
+        }
+    }
+#endif
 }
 #undef GGS_PAIR
 
@@ -803,3 +851,9 @@ hipError_t launch_finalize(hipStream_t st, const float* partials, const float* w
 }
 
 }  // namespace ggs
+
+#if GGS_TIMING
+extern "C" int ggs_debug_timing_read(void* host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(ggs::g_ggs_timing), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+#endif
