@@ -6,8 +6,9 @@ candidate, pop = 128 candidates per GPU, weighted-L2 fitness (the GA's default
 path, fitness.py:28-31 with the importance mask) — one *step* = one generation's
 evaluation: encode + preprocess + raster + fused weighted L2 + finalize for all
 128 candidates (libggs.so, device-pointer API, inputs resident in HBM), plus —
-for N > 1 GPUs — the RCCL all-gather of the fitness scalars (the only exchange
-step; candidates are sharded, weak scaling).
+for N > 1 GPUs — the RCCL all-gather of the fitness scalars (libggs
+ggs_comm_allgather on the compute stream; the only exchange step; candidates
+are sharded, weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -38,6 +39,16 @@ N_SPLATS = 256
 POP = 128
 K_SIGMA = 3.0
 N_POPS = 4
+RING = 4                         # in-flight fitness vectors (gather overlap)
+# How the per-batch fitness all-gather is issued (A/B switch, tools/gather_exp.sh;
+# "none" is a diagnostic, not a valid N>1 configuration):
+#   "rccl"         (default) libggs's RCCL communicator, in order on the compute
+#                  stream right after finalize: +1.5 us per step at world 1
+#   "rccl-overlap" the same on the communicator's own stream, joined through the
+#                  ring: +21 us (the cross-stream event waits cost more than they hide)
+#   "torch" / "torch-sync"  torch.distributed all_gather_into_tensor, async through
+#                  the ring / waited: +11 / +24 us
+GATHER = os.environ.get("GGS_BENCH_GATHER", "rccl")
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: peak FP32 vector
 FLOP_PER_PAIR = 24
@@ -174,8 +185,12 @@ def main():
             for i in range(N_POPS)]
     tgt = torch.from_numpy(tgt_h).to(dev)
     mask = torch.from_numpy(mask_h).to(dev)
-    out = torch.empty(POP, dtype=torch.float32, device=dev)
-    gathered = torch.empty(POP * world, dtype=torch.float32, device=dev)
+    # fitness vectors in a ring of slots: with an overlapped gather (A/B modes
+    # below) batch i's gather reads outs[i % RING] while batch i+1 is evaluated
+    # into the next slot; a slot is reused only after its gather (device-side wait)
+    outs = [torch.empty(POP, dtype=torch.float32, device=dev) for _ in range(RING)]
+    gathered = [torch.empty(POP * world, dtype=torch.float32, device=dev) for _ in range(RING)]
+    works = [None] * RING
     stream = torch.cuda.current_stream(dev)
     st = stream.cuda_stream
 
@@ -184,13 +199,34 @@ def main():
     plan = ggs.TargetPlan(local_rank, st, tgt.data_ptr(), mask.data_ptr(), ggs.GGS_FIT_WEIGHTED, 1.0,
                           H, W)
 
+    comm = ggs.RcclGather(local_rank) if distributed and GATHER.startswith("rccl") else None
+
+    def join(j):                                             # torch's stream waits for gather j
+        if works[j] is None:
+            return
+        if comm is not None:
+            comm.wait(st, works[j])
+        else:
+            works[j].wait()
+        works[j] = None
+
     def step(i):
-        g = pops[i % N_POPS]
-        plan.fitness_device(st, g.data_ptr(), POP, N_SPLATS, 9, K_SIGMA, out.data_ptr())
-        if distributed:
-            dist.all_gather_into_tensor(gathered, out)      # RCCL: fitness scalars to every rank
+        g, j = pops[i % N_POPS], i % RING
+        join(j)
+        plan.fitness_device(st, g.data_ptr(), POP, N_SPLATS, 9, K_SIGMA, outs[j].data_ptr())
+        if not distributed or GATHER == "none":
+            return
+        if comm is not None:                                 # RCCL: fitness scalars to every rank
+            works[j] = comm.allgather(st, outs[j].data_ptr(), gathered[j].data_ptr(), POP,
+                                      overlap=GATHER == "rccl-overlap")
+        else:
+            works[j] = dist.all_gather_into_tensor(gathered[j], outs[j], async_op=True)
+        if GATHER == "torch-sync":
+            join(j)
 
     def barrier():
+        for j in range(RING):
+            join(j)
         if distributed:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -201,12 +237,18 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    host_s = time.perf_counter() - t0                       # enqueue time (host side)
     barrier()
     elapsed = time.perf_counter() - t0
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    if distributed and GATHER != "none":                    # the gather delivered this rank's shard
+        j = (args.steps - 1) % RING
+        mine = gathered[j][rank * POP:(rank + 1) * POP]
+        assert torch.equal(mine, outs[j]), "fitness all-gather returned a different shard"
 
     # per-kernel device time (HIP events on the launch stream) over a second,
     # identical pass; the raster kernel is the dominant one
@@ -252,7 +294,8 @@ def main():
             "config": {"workload": f"{H}x{W} canvas, {N_SPLATS} splats/candidate, pop={POP} per GPU, "
                                    "weighted-L2 fitness (encode+prep+raster+reduce)",
                        "H": H, "W": W, "splats": N_SPLATS, "pop_per_gpu": POP,
-                       "global_batch": POP * world, "parallelism": f"dp{world} (candidate shards)"},
+                       "global_batch": POP * world, "parallelism": f"dp{world} (candidate shards)",
+                       "fitness_gather": (GATHER if distributed else None)},
             "gsplat_pixels_per_s": round(value * N_SPLATS * H * W / 1e9, 2),
             "aabb_pairs_per_s": round(value * pairs_per_cand, 1),
             "roofline": {"bound": "hbm", "kernel": "raster_kernel<1>",
@@ -269,10 +312,13 @@ def main():
                      "accounting": "reference-equivalent work: 24 FLOP per AABB pair (SURVEY.md §8d); "
                                    "the row recurrence executes fewer, so frac can exceed 1",
                      "busy_pmc": pmc_valu_busy() if args.config == "512" else None},
+            "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "kernels_ms_per_launch": {k: round(v[0] / max(v[1], 1), 5) for k, v in kern.items()},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if distributed:
         dist.destroy_process_group()
 

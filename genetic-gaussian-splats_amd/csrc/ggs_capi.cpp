@@ -40,6 +40,16 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+// thread-local ggs_last_error() message, for the other translation units (ggs_comm.cpp)
+int set_error(int code, const char* msg) {
+    t_err = msg ? msg : "";
+    return code;
+}
+
+namespace {
+
 #define GGS_HIP(call)                                                                            \
     do {                                                                                         \
         hipError_t e_ = (call);                                                                  \

@@ -1,0 +1,207 @@
+// Multi-GPU fitness gather over RCCL: candidates are sharded
+// across the GPUs of a node, one process per GPU, and the only exchange is an
+// all-gather of every rank's fitness scalars (xGMI).  The reference is
+// single-device (render.py:4, fitness.py:34-47 evaluates one list on one GPU);
+// this is the collective its sharded evaluation needs.
+//
+// The gather is enqueued by the library on the caller's stream (in order after
+// the fitness kernels) or on the communicator's own stream (overlap: the next
+// batch's raster runs while the scalars move).  RCCL is loaded at first use:
+// the copy already in the process when there is one (PyTorch bundles its own,
+// SONAME librccl.so.1, and ggs/_lib.py preloads it like the HIP runtime), else
+// $GGS_RCCL, else librccl.so.1 from the rpath (/opt/rocm/lib).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types and enums only; entry points are resolved by dlsym
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "../../include/ggs.h"
+
+namespace ggs {
+int set_error(int code, const char* msg);   // ggs_capi.cpp (thread-local ggs_last_error)
+namespace {
+
+int cfail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    return set_error(code, buf);
+}
+
+struct Rccl {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+    std::string err;
+    bool ok = false;
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h && getenv("GGS_RCCL")) h = dlopen(getenv("GGS_RCCL"), RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            r.err = std::string("cannot load RCCL (librccl.so.1): ") + (e ? e : "?");
+            return;
+        }
+        r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+        r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+        r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+        r.ok = r.get_unique_id && r.comm_init_rank && r.all_gather && r.comm_destroy && r.error_string;
+        if (!r.ok) r.err = "RCCL is missing an entry point (ncclGetUniqueId / ncclCommInitRank / "
+                           "ncclAllGather / ncclCommDestroy / ncclGetErrorString)";
+    });
+    return r;
+}
+
+#define GGS_NCCL(call)                                                                           \
+    do {                                                                                         \
+        ncclResult_t r_ = (call);                                                                \
+        if (r_ != ncclSuccess)                                                                   \
+            return cfail(GGS_EHIP, "%s: %s", #call, R.error_string(r_));                         \
+    } while (0)
+#define GGS_HIPC(call)                                                                           \
+    do {                                                                                         \
+        hipError_t e_ = (call);                                                                  \
+        if (e_ != hipSuccess) return cfail(GGS_EHIP, "%s: %s", #call, hipGetErrorString(e_));    \
+    } while (0)
+
+constexpr int kTickets = 64;   // gathers a caller may still wait on
+
+struct Comm {
+    int dev = 0, nranks = 1, rank = 0;
+    ncclComm_t nc = nullptr;
+    hipStream_t side = nullptr;          // overlap mode: gathers run here
+    hipEvent_t ready = nullptr;          // caller's stream -> side
+    hipEvent_t done[kTickets] = {};      // side -> caller's stream, one per ticket slot
+    int64_t issued = 0;                  // tickets handed out
+    std::mutex mu;
+};
+
+struct DevScope {
+    int prev = -1;
+    explicit DevScope(int d) { if (hipGetDevice(&prev) != hipSuccess) prev = -1; (void)hipSetDevice(d); }
+    ~DevScope() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+}  // namespace
+}  // namespace ggs
+
+using namespace ggs;
+
+extern "C" {
+
+int ggs_comm_unique_id(uint8_t* id128) {
+    const Rccl& R = rccl();
+    if (!R.ok) return cfail(GGS_ENODEV, "%s", R.err.c_str());
+    if (!id128) return cfail(GGS_EINVAL, "ggs_comm_unique_id: null output");
+    static_assert(sizeof(ncclUniqueId) == GGS_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    GGS_NCCL(R.get_unique_id(&u));
+    memcpy(id128, &u, sizeof u);
+    return GGS_OK;
+}
+
+int ggs_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* id128, void** comm) {
+    const Rccl& R = rccl();
+    if (!R.ok) return cfail(GGS_ENODEV, "%s", R.err.c_str());
+    if (!comm || !id128 || nranks < 1 || rank < 0 || rank >= nranks)
+        return cfail(GGS_EINVAL, "ggs_comm_create: need 0 <= rank (%d) < nranks (%d), id and comm", rank, nranks);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return cfail(GGS_ENODEV, "ggs_comm_create: device %d not available (%d visible)", device, ndev);
+    DevScope ds(device);
+    Comm* c = new Comm;
+    c->dev = device;
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclUniqueId u;
+    memcpy(&u, id128, sizeof u);
+    int rc = GGS_OK;
+    ncclResult_t nr = R.comm_init_rank(&c->nc, nranks, u, rank);
+    if (nr != ncclSuccess) rc = cfail(GGS_EHIP, "ncclCommInitRank: %s", R.error_string(nr));
+    hipError_t he = hipSuccess;
+    if (!rc) he = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (!rc && he == hipSuccess) he = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
+    for (int i = 0; !rc && he == hipSuccess && i < kTickets; ++i)
+        he = hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming);
+    if (!rc && he != hipSuccess) rc = cfail(GGS_EHIP, "ggs_comm_create: %s", hipGetErrorString(he));
+    if (rc) {
+        ggs_comm_destroy(c);
+        return rc;
+    }
+    *comm = c;
+    return GGS_OK;
+}
+
+int ggs_comm_allgather(void* comm, void* stream, const float* d_send, float* d_recv, int64_t count,
+                       int32_t overlap, int64_t* ticket) {
+    const Rccl& R = rccl();
+    Comm* c = (Comm*)comm;
+    if (!c || !R.ok) return cfail(GGS_EINVAL, "ggs_comm_allgather: no communicator");
+    if (count < 0 || (count > 0 && (!d_send || !d_recv)))
+        return cfail(GGS_EINVAL, "ggs_comm_allgather: count %lld with null buffers", (long long)count);
+    std::lock_guard<std::mutex> lk(c->mu);
+    DevScope ds(c->dev);
+    hipStream_t st = (hipStream_t)stream;
+    if (!overlap) {
+        GGS_NCCL(R.all_gather(d_send, d_recv, (size_t)count, ncclFloat32, c->nc, st));
+        if (ticket) *ticket = -1;
+        return GGS_OK;
+    }
+    // overlap: the gather waits for the work already on `stream` (the fitness
+    // kernels that wrote d_send), then runs on the side stream
+    GGS_HIPC(hipEventRecord(c->ready, st));
+    GGS_HIPC(hipStreamWaitEvent(c->side, c->ready, 0));
+    GGS_NCCL(R.all_gather(d_send, d_recv, (size_t)count, ncclFloat32, c->nc, c->side));
+    const int64_t t = c->issued++;
+    GGS_HIPC(hipEventRecord(c->done[t % kTickets], c->side));
+    if (ticket) *ticket = t;
+    return GGS_OK;
+}
+
+int ggs_comm_wait(void* comm, void* stream, int64_t ticket) {
+    Comm* c = (Comm*)comm;
+    if (!c) return cfail(GGS_EINVAL, "ggs_comm_wait: no communicator");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (ticket < 0) return GGS_OK;                       // in-stream gather: nothing to join
+    if (ticket >= c->issued) return cfail(GGS_EINVAL, "ggs_comm_wait: ticket %lld not issued", (long long)ticket);
+    DevScope ds(c->dev);
+    // a slot reused by a later ticket still orders after `ticket` (one side stream)
+    GGS_HIPC(hipStreamWaitEvent((hipStream_t)stream, c->done[ticket % kTickets], 0));
+    return GGS_OK;
+}
+
+void ggs_comm_destroy(void* comm) {
+    Comm* c = (Comm*)comm;
+    if (!c) return;
+    const Rccl& R = rccl();
+    {
+        DevScope ds(c->dev);
+        if (c->side) (void)hipStreamSynchronize(c->side);
+        if (c->nc && R.ok) (void)R.comm_destroy(c->nc);
+        for (int i = 0; i < kTickets; ++i)
+            if (c->done[i]) (void)hipEventDestroy(c->done[i]);
+        if (c->ready) (void)hipEventDestroy(c->ready);
+        if (c->side) (void)hipStreamDestroy(c->side);
+    }
+    delete c;
+}
+
+}  // extern "C"

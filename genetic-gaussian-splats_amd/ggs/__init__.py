@@ -6,6 +6,7 @@ include/ggs.h).  The drop-in modules with the reference's names live in
 """
 from ._lib import (GGS_FIT_BOOST, GGS_FIT_NONE, GGS_FIT_WEIGHTED, GGSDeviceError,  # noqa: F401
                    GGSError, GGSInputError, LIB_PATH, ensure_init, lib, select_devices)
+from .parallel import RcclGather  # noqa: F401
 from .api import (TargetPlan, as_f32, encode, fitness, fitness_device,  # noqa: F401
                   fitness_population, preprocess, profile_enable, profile_read, profile_reset,
                   render, render_device)

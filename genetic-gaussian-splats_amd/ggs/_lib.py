@@ -84,6 +84,13 @@ SIGNATURES = {
     "ggs_sa_destroy": (None, [C.c_void_p]),
     "ggs_sa_set_incremental": (C.c_int, [C.c_void_p, C.c_int32]),
     "ggs_sa_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "ggs_comm_unique_id": (C.c_int, [C.c_void_p]),
+    "ggs_comm_create": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                  C.POINTER(C.c_void_p)]),
+    "ggs_comm_allgather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                     C.c_int32, C.POINTER(C.c_int64)]),
+    "ggs_comm_wait": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "ggs_comm_destroy": (None, [C.c_void_p]),
 }
 
 
@@ -125,6 +132,24 @@ def _share_hip_runtime_with_torch() -> None:
             p = os.path.join(tlib, dep)
             if os.path.exists(p):
                 C.CDLL(p, mode=C.RTLD_GLOBAL)
+
+
+def preload_rccl() -> None:
+    """Same rule for RCCL (ggs_comm_*): PyTorch bundles its own librccl with the
+    SONAME of /opt/rocm's; load torch's first so libggs's dlopen finds the copy
+    torch.distributed uses.  Called before the first communicator is made."""
+    if os.environ.get("GGS_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    p = os.path.join(list(spec.submodule_search_locations)[0], "lib", "librccl.so")
+    if os.path.exists(p):
+        C.CDLL(p, mode=C.RTLD_GLOBAL)
 
 
 def _load() -> C.CDLL:

@@ -78,3 +78,56 @@ class ShardedFitness:
         b0, b1 = shard_bounds(B, self.world, self.rank)
         local = np.asarray(self.evaluate(G[b0:b1]), np.float32) if b1 > b0 else np.zeros(0, np.float32)
         return gather_shards(local, B, self.group, self.device)
+
+
+class RcclGather:
+    """All-gather of each rank's fitness scalars over RCCL, issued by libggs on a
+    HIP stream (``ggs_comm_*``, include/ggs.h) — the data-path collective of the
+    sharded evaluation.  ``torch.distributed`` (any backend) only carries the
+    128-byte communicator id from rank 0 to the others.
+
+    ``allgather(stream, d_send, d_recv, count, overlap)`` takes device pointers;
+    with ``overlap=True`` it returns a ticket and the gather runs on the
+    communicator's own stream; ``wait(stream, ticket)`` joins it back (device-side).
+    """
+
+    def __init__(self, device: int, group=None):
+        import ctypes as C
+        import torch.distributed as dist
+        from . import _lib
+        _lib.preload_rccl()
+        self._lib, self._C = _lib, C
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        idb = (C.c_uint8 * 128)()
+        if self.rank == 0:
+            _lib.check(_lib.lib.ggs_comm_unique_id(idb), "ggs_comm_unique_id")
+        box = [bytes(idb)]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group)
+        idb = (C.c_uint8 * 128).from_buffer_copy(box[0])
+        h = C.c_void_p()
+        _lib.check(_lib.lib.ggs_comm_create(int(device), self.world, self.rank, idb, C.byref(h)),
+                   "ggs_comm_create")
+        self.handle = h
+
+    def allgather(self, stream: int, d_send: int, d_recv: int, count: int, overlap: bool = False) -> int:
+        t = self._C.c_int64(-1)
+        self._lib.check(self._lib.lib.ggs_comm_allgather(self.handle, stream, d_send, d_recv, int(count),
+                                                         int(bool(overlap)), self._C.byref(t)),
+                        "ggs_comm_allgather")
+        return t.value
+
+    def wait(self, stream: int, ticket: int) -> None:
+        self._lib.check(self._lib.lib.ggs_comm_wait(self.handle, stream, int(ticket)), "ggs_comm_wait")
+
+    def close(self) -> None:
+        if self.handle:
+            self._lib.lib.ggs_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -195,6 +195,28 @@ int ggs_sa_set_incremental(void* handle, int32_t on);
 int ggs_sa_stats(void* handle, uint64_t* proposed, uint64_t* changed_splats);
 void ggs_sa_destroy(void* handle);
 
+/* ---- multi-GPU fitness gather -------------------------------
+ * One process per GPU; candidates are sharded in contiguous blocks and the only
+ * exchange is an all-gather of each rank's fitness scalars over RCCL (xGMI).
+ * Replaces nothing in the reference (single-device, render.py:4); it is the
+ * collective of the sharded fitness_population (fitness.py:34-47).  RCCL is
+ * loaded at first use (the copy already in the process, else $GGS_RCCL, else
+ * librccl.so.1).  Rank 0 makes the id, every rank passes the same bytes. */
+#define GGS_COMM_ID_BYTES 128
+int ggs_comm_unique_id(uint8_t* id128);
+int ggs_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* id128, void** comm);
+/* recv[r*count + i] = rank r's send[i] (device pointers).  overlap = 0: enqueued
+ * on `stream` after the work already there; *ticket = -1.  overlap = 1: runs on
+ * the communicator's own stream once the work already on `stream` is done, and
+ * `stream` continues at once; *ticket names it for ggs_comm_wait (the caller
+ * must not overwrite d_send or read d_recv before waiting). */
+int ggs_comm_allgather(void* comm, void* stream, const float* d_send, float* d_recv, int64_t count,
+                       int32_t overlap, int64_t* ticket);
+/* Make `stream` wait (on the device, no host sync) for the gather `ticket`;
+ * valid for the 64 most recent tickets. */
+int ggs_comm_wait(void* comm, void* stream, int64_t ticket);
+void ggs_comm_destroy(void* comm);
+
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------
  * When enabled, every launch of "prep", "raster" and "finalize" is bracketed
  * by hipEvents; ggs_profile_read synchronises those events and returns the
