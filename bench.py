@@ -49,6 +49,18 @@ RING = 4                         # in-flight fitness vectors (gather overlap)
 #   "torch" / "torch-sync"  torch.distributed all_gather_into_tensor, async through
 #                  the ring / waited: +11 / +24 us
 GATHER = os.environ.get("GGS_BENCH_GATHER", "rccl")
+# Consecutive batches are independent populations, so they alternate over two
+# HIP streams: one batch's raster fills the CUs the other's grid tail (and its
+# prep/finalize launches) leave idle — tools/streams_exp.sh: 0.189 -> 0.173 ms
+# per batch.  A GA generation depends on the previous one's fitness and runs at
+# the one-stream rate, reported beside as value_one_stream.
+STREAMS = int(os.environ.get("GGS_BENCH_STREAMS", "2"))
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); under
+# torchrun torch's and RCCL's streams take queues too and the second compute
+# stream ends up sharing one (669k vs 730k renders/s at world 1), so ask for 8.
+# Read by the HIP runtime at initialisation, which happens after this line.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: peak FP32 vector
 FLOP_PER_PAIR = 24
@@ -150,10 +162,12 @@ def _cpu_model() -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="512")
+    ap.add_argument("--streams", type=int, default=STREAMS,
+                    help="HIP streams the independent batches alternate over (1 = dependent batches)")
     args = ap.parse_args()
     global H, W, N_SPLATS, POP
     H, N_SPLATS, POP = CONFIGS[args.config]
@@ -193,32 +207,43 @@ def main():
     works = [None] * RING
     stream = torch.cuda.current_stream(dev)
     st = stream.cuda_stream
+    # batches alternate over STREAMS HIP streams (independent batches: the next
+    # batch's raster fills the CUs the previous one's grid tail leaves idle)
+    assert RING % args.streams == 0, f"--streams must divide {RING}"
+    assert args.streams == 1 or not (distributed and GATHER.startswith("torch")), \
+        "torch.distributed gathers run on torch's current stream: use --streams 1"
+    sts = [st] + [torch.cuda.Stream(dev).cuda_stream for _ in range(args.streams - 1)]
 
     # the target/mask are fixed over a GA run: lay them out once for the raster's
     # fitness epilogue (ggs_plan_create), as the device-resident GA does
     plan = ggs.TargetPlan(local_rank, st, tgt.data_ptr(), mask.data_ptr(), ggs.GGS_FIT_WEIGHTED, 1.0,
                           H, W)
 
-    comm = ggs.RcclGather(local_rank) if distributed and GATHER.startswith("rccl") else None
+    # one RCCL communicator per stream: a communicator orders its collectives
+    # across streams, which would serialise the alternating batches again
+    comms = [ggs.RcclGather(local_rank) for _ in range(args.streams)] \
+        if distributed and GATHER.startswith("rccl") else None
+    comm = comms[0] if comms else None
 
-    def join(j):                                             # torch's stream waits for gather j
+    def join(j):                                             # slot j's stream waits for its gather
         if works[j] is None:
             return
         if comm is not None:
-            comm.wait(st, works[j])
+            k, ticket = works[j]                             # (stream/communicator index, ticket)
+            comms[k].wait(sts[k], ticket)
         else:
             works[j].wait()
         works[j] = None
 
-    def step(i):
-        g, j = pops[i % N_POPS], i % RING
+    def step(i, ns):
+        g, j, st = pops[i % N_POPS], i % RING, sts[i % ns]
         join(j)
         plan.fitness_device(st, g.data_ptr(), POP, N_SPLATS, 9, K_SIGMA, outs[j].data_ptr())
         if not distributed or GATHER == "none":
             return
         if comm is not None:                                 # RCCL: fitness scalars to every rank
-            works[j] = comm.allgather(st, outs[j].data_ptr(), gathered[j].data_ptr(), POP,
-                                      overlap=GATHER == "rccl-overlap")
+            works[j] = (i % ns, comms[i % ns].allgather(st, outs[j].data_ptr(), gathered[j].data_ptr(), POP,
+                                                        overlap=GATHER == "rccl-overlap"))
         else:
             works[j] = dist.all_gather_into_tensor(gathered[j], outs[j], async_op=True)
         if GATHER == "torch-sync":
@@ -231,31 +256,38 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for i in range(args.warmup):
-        step(i)
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    host_s = time.perf_counter() - t0                       # enqueue time (host side)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(ns):
+        """W untimed + K timed steps over ns streams: (max-over-ranks seconds, host enqueue s)."""
+        for i in range(args.warmup):
+            step(i, ns)
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(i, ns)
+        host_s = time.perf_counter() - t0                   # enqueue time (host side)
+        barrier()
+        el = time.perf_counter() - t0
+        if distributed:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, host_s
 
+    elapsed, host_s = timed(args.streams)                  # the headline
     if distributed and GATHER != "none":                    # the gather delivered this rank's shard
         j = (args.steps - 1) % RING
         mine = gathered[j][rank * POP:(rank + 1) * POP]
         assert torch.equal(mine, outs[j]), "fitness all-gather returned a different shard"
+    # dependent batches (a GA generation needs the previous one's fitness): one stream
+    elapsed1, _ = timed(1) if args.streams > 1 else (elapsed, host_s)
 
-    # per-kernel device time (HIP events on the launch stream) over a second,
-    # identical pass; the raster kernel is the dominant one
+    # per-kernel device time (HIP events on the launch stream) over a third,
+    # single-stream pass (kernels alone, not sharing the chip with the other
+    # stream's): the raster kernel is the dominant one
     ggs.profile_reset()
     ggs.profile_enable(True)
     for i in range(args.steps):
-        step(i)
+        step(i, 1)
     barrier()
     ggs.profile_enable(False)
     kern = {k: ggs.profile_read(k) for k in ("prep", "raster", "finalize")}
@@ -312,13 +344,15 @@ def main():
                      "accounting": "reference-equivalent work: 24 FLOP per AABB pair (SURVEY.md §8d); "
                                    "the row recurrence executes fewer, so frac can exceed 1",
                      "busy_pmc": pmc_valu_busy() if args.config == "512" else None},
+            "streams": args.streams,
+            "value_one_stream": round(world * POP * args.steps / elapsed1, 1),
             "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "kernels_ms_per_launch": {k: round(v[0] / max(v[1], 1), 5) for k, v in kern.items()},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if comm is not None:
-        comm.close()
+    for c in comms or ():
+        c.close()
     if distributed:
         dist.destroy_process_group()
 

@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 
@@ -94,6 +95,14 @@ struct Comm {
     std::mutex mu;
 };
 
+// A gather over one rank is a copy: done by a small kernel on the stream, not
+// through RCCL (whose single-rank path costs a stream-ordering round trip).
+__global__ void __launch_bounds__(256) copy_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                   int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 struct DevScope {
     int prev = -1;
     explicit DevScope(int d) { if (hipGetDevice(&prev) != hipSuccess) prev = -1; (void)hipSetDevice(d); }
@@ -160,6 +169,15 @@ int ggs_comm_allgather(void* comm, void* stream, const float* d_send, float* d_r
     std::lock_guard<std::mutex> lk(c->mu);
     DevScope ds(c->dev);
     hipStream_t st = (hipStream_t)stream;
+    if (c->nranks == 1 && !overlap && !getenv("GGS_COMM_RCCL_SELF")) {
+        if (count > 0 && d_send != d_recv) {
+            const unsigned grid = (unsigned)std::min<int64_t>((count + 255) / 256, 1024);
+            hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, st, d_send, d_recv, count);
+            GGS_HIPC(hipGetLastError());
+        }
+        if (ticket) *ticket = -1;
+        return GGS_OK;
+    }
     if (!overlap) {
         GGS_NCCL(R.all_gather(d_send, d_recv, (size_t)count, ncclFloat32, c->nc, st));
         if (ticket) *ticket = -1;

@@ -13,6 +13,18 @@ if os.path.exists(stats):
             "calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
             "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3,
             "pct": float(r["Percentage"])}
+# bench.py's last pass is single-stream with per-launch HIP events (the live
+# avg_launch_ms): average the raster over its dispatches alone (the last STEPS)
+# and over the two-stream timed pass (the first STEPS after warm-up)
+trace = os.path.join(root, "trace", "run_kernel_trace.csv")
+steps = int(os.environ.get("PROF_STEPS", "30"))
+if os.path.exists(trace):
+    rows = [r for r in csv.DictReader(open(trace)) if "raster_kernel" in r.get("Kernel_Name", "")]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+    if len(dur) >= steps:
+        out["raster_profile_pass_avg_us"] = sum(dur[-steps:]) / steps
+        out["raster_dispatches"] = len(dur)
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(root, "pmc_*", "run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
