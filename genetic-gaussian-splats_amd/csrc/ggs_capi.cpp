@@ -442,7 +442,7 @@ void ggs_shutdown(void) {
         (void)hipStreamSynchronize(c->stream);
         for (auto& w : c->ws) {
             if (w->stream) (void)hipStreamSynchronize(w->stream);
-            for (DevBuf* b : {&w->recs, &w->partials, &w->wpartials, &w->order})
+            for (DevBuf* b : {&w->recs, &w->partials, &w->wpartials, &w->order, &w->plan})
                 if (b->p) (void)hipFree(b->p);
         }
         for (DevBuf* b : {&c->gen, &c->out, &c->target, &c->mask})
