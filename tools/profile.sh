@@ -1,5 +1,5 @@
 #!/bin/bash
-# rocprofv3 passes over the bench workload (512x512 / 256 splats / pop 128):
+# rocprofv3 passes over a workload (default: the bench, 512x512 / 256 splats / pop 128):
 #   1. --kernel-trace --stats           -> per-kernel durations
 #   2. --pmc FETCH_SIZE                 -> HBM read bytes   (own pass)
 #   3. --pmc WRITE_SIZE                 -> HBM write bytes  (own pass)
@@ -11,7 +11,9 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline"
+# the profiled command (default: the bench workload); another config:
+#   BENCH="python3 bench.py --config 1024 --steps 10 --warmup 2 --no-cpu-baseline" PROF_STEPS=10 tools/profile.sh r01_1024
+BENCH=${BENCH:-"python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline"}
 run() { local name=$1; shift; echo "== $name: $*" | tee -a "$OUT/commands.txt"; timeout -k 10 300 "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }; }
 run trace rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- $BENCH
 run pmc_fetch rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- $BENCH
