@@ -292,6 +292,28 @@ def test_target_cache_sees_content_change(full_size):
     np.testing.assert_array_equal(ggs.fitness(pop[:4], tgt, H, W, 3.0, weight_mask=mask), a)
 
 
+def test_full_size_two_streams_concurrent_bit_identical(full_size):
+    """bench.py's schedule: batches alternate over two HIP streams (one workspace
+    each) with both in flight at once; every batch's fitness has the same bits as
+    the host API's serial evaluation."""
+    torch = pytest.importorskip("torch")
+    pop, tgt, mask, H, W = full_size
+    dev = torch.device("cuda:0")
+    ref = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+    g = torch.from_numpy(pop).to(dev)
+    t_d, m_d = torch.from_numpy(tgt).to(dev), torch.from_numpy(mask).to(dev)
+    sts = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    plan = ggs.TargetPlan(0, sts[0].cuda_stream, t_d.data_ptr(), m_d.data_ptr(), ggs.GGS_FIT_WEIGHTED, 1.0,
+                          H, W)
+    torch.cuda.synchronize(dev)
+    outs = [torch.empty(len(pop), device=dev) for _ in range(8)]
+    for i, o in enumerate(outs):
+        plan.fitness_device(sts[i % 2].cuda_stream, g.data_ptr(), len(pop), pop.shape[1], 9, 3.0, o.data_ptr())
+    torch.cuda.synchronize(dev)
+    for o in outs:
+        np.testing.assert_array_equal(o.cpu().numpy(), ref)
+
+
 # ---- device-pointer API (inputs resident in HBM) ---------------------------------------------
 def test_device_api_matches_host_api(full_size):
     torch = pytest.importorskip("torch")
