@@ -807,6 +807,8 @@ struct GaSession {
         best_upd, curves, draws;
     DevBuf recs, partials, plan, wpart, order;   // the generation's fused pipeline
     int64_t n_curves = 0, curves_cap = 0;
+    void* comm = nullptr;          // ggs_ga_set_comm: offspring fitness sharded over ranks
+    int nranks = 1, rank = 0;
 };
 
 double anneal_factor(int gen, int total, int kind) {          // utils.py:14-27
@@ -917,15 +919,27 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     }
 #endif
     const float bg[3] = {1.f, 1.f, 1.f};
-    {
-        ProfScope ps(s->st, 1);
-        GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->recs.p, P, N, c.H, c.W, bg, nullptr,
-                              (const float4*)s->plan.p, (float*)s->partials.p, (const int*)s->order.p));
+    // this rank's contiguous shard of the offspring (all of them on one GPU);
+    // every rank bred all P offspring above with the same draws
+    const int per = (P + s->nranks - 1) / s->nranks;
+    const int b0 = std::min(P, s->rank * per), nb = std::min(P, b0 + per) - b0;
+    if (nb > 0) {
+        {
+            ProfScope ps(s->st, 1);
+            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->recs.p + (int64_t)b0 * N, nb, N, c.H, c.W, bg,
+                                  nullptr, (const float4*)s->plan.p, (float*)s->partials.p,
+                                  (const int*)s->order.p));
+        }
+        {
+            ProfScope ps(s->st, 2);
+            GGS_HIP(launch_finalize(s->st, (const float*)s->partials.p, (const float*)s->wpart.p, nb,
+                                    s->nTiles, c.fitness_mode, c.H, c.W, (float*)s->off_fits.p + b0));
+        }
     }
-    {
-        ProfScope ps(s->st, 2);
-        GGS_HIP(launch_finalize(s->st, (const float*)s->partials.p, (const float*)s->wpart.p, P, s->nTiles,
-                                c.fitness_mode, c.H, c.W, (float*)s->off_fits.p));
+    if (s->comm) {   // one in-place all-gather of the shards' fitness scalars (RCCL, same stream)
+        float* of = (float*)s->off_fits.p;
+        if ((rc = ggs_comm_allgather(s->comm, s->st, of + (int64_t)s->rank * per, of, per, 0, nullptr)))
+            return rc;
     }
     double* row;
     if ((rc = ga_curves_row(s, &row))) return rc;
@@ -1094,6 +1108,25 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
         return bail(fail(GGS_EHIP, "initial evaluation failed"));
     s->n_curves = 1;
     *handle = s.release();
+    return GGS_OK;
+}
+
+int ggs_ga_set_comm(void* handle, void* comm) {
+    GaSession* s = (GaSession*)handle;
+    if (!s) return fail(GGS_EINVAL, "null GA handle");
+    int32_t n = 1, r = 0;
+    if (comm) {
+        int rc = ggs_comm_size(comm, &n, &r);
+        if (rc) return rc;
+    }
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    DeviceGuard dg(s->c->dev);
+    const int per = (s->P + n - 1) / n;
+    int rc = ensure(s->off_fits, sizeof(float) * (size_t)per * n, s->st);   // gather target: n shards
+    if (rc) return rc;
+    s->comm = comm;
+    s->nranks = n;
+    s->rank = r;
     return GGS_OK;
 }
 

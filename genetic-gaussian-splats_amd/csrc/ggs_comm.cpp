@@ -206,6 +206,14 @@ int ggs_comm_wait(void* comm, void* stream, int64_t ticket) {
     return GGS_OK;
 }
 
+int ggs_comm_size(void* comm, int32_t* nranks, int32_t* rank) {
+    Comm* c = (Comm*)comm;
+    if (!c) return cfail(GGS_EINVAL, "ggs_comm_size: no communicator");
+    if (nranks) *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+    return GGS_OK;
+}
+
 void ggs_comm_destroy(void* comm) {
     Comm* c = (Comm*)comm;
     if (!c) return;

@@ -90,7 +90,9 @@ SIGNATURES = {
     "ggs_comm_allgather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                      C.c_int32, C.POINTER(C.c_int64)]),
     "ggs_comm_wait": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "ggs_comm_size": (C.c_int, [C.c_void_p, _i32p, _i32p]),
     "ggs_comm_destroy": (None, [C.c_void_p]),
+    "ggs_ga_set_comm": (C.c_int, [C.c_void_p, C.c_void_p]),
 }
 
 

@@ -150,6 +150,13 @@ class DeviceGA:
                                 pop.ctypes.data_as(_f32p), C.byref(h)), "ggs_ga_create")
         self.h = h
 
+    def set_comm(self, gather) -> None:
+        """Shard each generation's offspring evaluation over the ranks of an
+        ``ggs.RcclGather`` (one process per GPU, identical sessions on every rank;
+        ggs_ga_set_comm).  ``None``: evaluate every offspring here."""
+        self._comm = gather                     # keeps the communicator alive
+        check(lib.ggs_ga_set_comm(self.h, None if gather is None else gather.handle), "ggs_ga_set_comm")
+
     def step(self, gen: int, total: int, draws: Optional[Dict[str, np.ndarray]] = None) -> None:
         """One generation; ``draws`` in ggs/ga.py layout (see draws_from_host)."""
         if draws is None:

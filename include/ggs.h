@@ -162,6 +162,16 @@ typedef struct ggs_ga_draws {         /* host arrays for ONE generation (ggs/ga.
  * GGS_FIT_NONE.  Evaluates the initial population. */
 int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_hw3,
                   const float* mask_hw, const float* init_pop, void** handle);
+/* Shard the device GA's fitness evaluation over the ranks of `comm` (one
+ * process per GPU; every rank created its session with the same config, target,
+ * mask, initial population and seed, and steps it with the same arguments):
+ * each generation every rank breeds all P offspring (same draws), rasterises its
+ * contiguous block of ceil(P/nranks), and one in-place RCCL all-gather of the
+ * offspring fitness scalars lets every rank run the same survivors step, so the
+ * populations stay identical without exchanging genomes (north_star: shard the
+ * generation's candidates across the GPUs of a node).  comm = NULL: one GPU.
+ * The communicator must outlive the session's use of it. */
+int ggs_ga_set_comm(void* handle, void* comm);
 int ggs_ga_step(void* handle, int32_t gen, int32_t total_gens, const ggs_ga_draws* draws);
 int ggs_ga_run(void* handle, int32_t first_gen, int32_t n_gens, int32_t total_gens);
 /* Synchronises; any output may be NULL.  curves: [n_curves][3] = best, mean, median. */
@@ -215,6 +225,7 @@ int ggs_comm_allgather(void* comm, void* stream, const float* d_send, float* d_r
 /* Make `stream` wait (on the device, no host sync) for the gather `ticket`;
  * valid for the 64 most recent tickets. */
 int ggs_comm_wait(void* comm, void* stream, int64_t ticket);
+int ggs_comm_size(void* comm, int32_t* nranks, int32_t* rank);
 void ggs_comm_destroy(void* comm);
 
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------

@@ -85,3 +85,39 @@ def test_comm_argument_errors():
         ggs._lib.check(ggs.lib.ggs_comm_create(0, 2, 5, idb, C.byref(h)), "ggs_comm_create")
     with pytest.raises(ggs.GGSInputError):
         ggs._lib.check(ggs.lib.ggs_comm_wait(None, None, 0), "ggs_comm_wait")
+
+
+@pytest.mark.parametrize("via", ["copy", "rccl"])
+def test_device_ga_sharded_over_world1_comm_is_the_plain_ga(world1, via, monkeypatch):
+    """ggs_ga_set_comm: breed all, evaluate this rank's shard, all-gather the
+    fitness scalars — at world 1 the whole generation, bit-identical to the
+    unsharded session (populations, fitness, best, curves).  "rccl" routes the
+    single-rank gather through RCCL's in-place all-gather instead of the copy."""
+    if via == "rccl":
+        monkeypatch.setenv("GGS_COMM_RCCL_SELF", "1")
+    from ggs import ga
+    from ggs.ga_device import DeviceGA
+    H = W = 64
+    rng = np.random.default_rng(5)
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0.4, 1.0, (H, W)).astype(np.float32)
+    init = ga.new_population(24, 16, H, W, 3.0, 0.1, np.random.default_rng(2))
+    cfg = dict(tour_k=2, elite_k=4, cxpb=0.3, mutpb=0.2, min_scale_splats=3.0, max_scale_splats=0.1,
+               seed=9, schedule="cosine",
+               mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0, "alpha": 25.0},
+               mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0, "alpha": 2.0})
+    res = []
+    for shard in (False, True):
+        d = DeviceGA(tgt, mask, init, **cfg)
+        comm = ggs.RcclGather(0) if shard else None
+        if shard:
+            d.set_comm(comm)
+        d.run(1, 12, 12)
+        res.append(d.read())
+        d.close()
+        if comm is not None:
+            comm.close()
+    a, b = res
+    np.testing.assert_array_equal(a["population"], b["population"])
+    np.testing.assert_array_equal(a["fitness"], b["fitness"])
+    assert a["best_fit"] == b["best_fit"] and a["curves"] == b["curves"]

@@ -6,7 +6,9 @@ libggs launch per generation — with the host/device split.
 on the GPU (Philox draws), timed around DeviceGA.run + a final read.
 
 usage: python tools/bench_ga.py [--gens 200] [--pop 128] [--splats 256] [--size 512]
-                                [--backend host|device]"""
+                                [--backend host|device]
+       python -m torch.distributed.run --nproc-per-node G tools/bench_ga.py --backend device ...
+           (configs[3]: --size 1024 --splats 1024 --pop 4096; offspring sharded over G GPUs)"""
 import argparse, json, os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -32,22 +34,50 @@ t = prepare_target(target, H, W)
 m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
 
 if a.backend == "device":
+    # under torch.distributed.run: one process per GPU, every rank runs the same
+    # session and evaluates its shard of the offspring; one RCCL all-gather of the
+    # fitness scalars per generation (ggs_ga_set_comm)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from ggs.ga_device import DeviceGA
     init = ga.new_population(a.pop, a.splats, H, W, 3.0, 0.1, np.random.default_rng(0))
     dga = DeviceGA(t, m, init, tour_k=2, elite_k=8, cxpb=0.05, mutpb=0.05, min_scale_splats=3.0,
-                   max_scale_splats=0.1, seed=1, **cfg)
+                   max_scale_splats=0.1, seed=1, device=local, **cfg)
+    gather = None
+    if dist is not None:
+        gather = ggs.RcclGather(local)
+        dga.set_comm(gather)
     dga.run(1, 5, a.gens)                                          # warm-up
     dga.read()
+    if dist is not None:
+        dist.barrier()
     t0 = time.perf_counter()
     dga.run(6, a.gens, a.gens + 5)
     st = dga.read()
     dt = time.perf_counter() - t0
-    print(json.dumps({"metric": "GA generations/s (device-resident)", "value": round(a.gens / dt, 2),
-                      "config": {"H": H, "W": W, "splats": a.splats, "pop": a.pop, "gens": a.gens},
-                      "ms_per_gen": round(dt / a.gens * 1e3, 4),
-                      "candidate_renders_per_s": round(a.gens * a.pop / dt, 1),
-                      "best_fit": st["best_fit"]}))
+    if dist is not None:                                           # max over ranks; same GA everywhere
+        out = [None] * world
+        dist.all_gather_object(out, (dt, st["best_fit"], float(st["fitness"].sum())))
+        dt = max(o[0] for o in out)
+        assert len({o[1:] for o in out}) == 1, f"ranks diverged: {out}"
+    if rank == 0:
+        print(json.dumps({"metric": "GA generations/s (device-resident)", "value": round(a.gens / dt, 2),
+                          "config": {"H": H, "W": W, "splats": a.splats, "pop": a.pop, "gens": a.gens,
+                                     "n_gpus": world, "sharded": dist is not None},
+                          "ms_per_gen": round(dt / a.gens * 1e3, 4),
+                          "candidate_renders_per_s": round(a.gens * a.pop / dt, 1),
+                          "best_fit": st["best_fit"]}))
     dga.close()
+    if gather is not None:
+        gather.close()
+    if dist is not None:
+        dist.destroy_process_group()
     sys.exit(0)
 
 
