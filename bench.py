@@ -3,14 +3,16 @@
 
 Workload (BASELINE.json `metric`, configs[1]): 512x512 canvas, 256 splats per
 candidate, pop = 128 candidates per GPU, weighted-L2 fitness (the GA's default
-path, fitness.py:28-31 with the importance mask) — one *step* = one generation's
-evaluation: encode + preprocess + raster + fused weighted L2 + finalize for all
-128 candidates (libggs.so, device-pointer API, inputs resident in HBM), plus —
-for N > 1 GPUs — the RCCL all-gather of the fitness scalars (libggs
+path, fitness.py:28-31 with the importance mask) — one *step* = the evaluation
+of one population of 128 candidates per GPU: encode + preprocess + raster + fused
+weighted L2 + finalize (libggs.so, device-pointer API, inputs resident in HBM),
+plus — for N > 1 GPUs — the RCCL all-gather of the fitness scalars (libggs
 ggs_comm_allgather on the compute stream; the only exchange step; candidates
-are sharded, weak scaling).
+are sharded, weak scaling).  Consecutive populations are independent and
+alternate over --streams HIP streams (default 2); `value_one_stream` is the rate
+when each step must wait for the previous one (a GA generation).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S] [--config 512|1024]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line.  Synthetic data: genomes drawn from the
