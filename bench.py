@@ -113,9 +113,10 @@ def pmc_valu_busy():
     if not paths:
         return None
     try:
-        c = json.load(open(paths[-1]))["counters"]["void ggs::raster_kernel<1>"]
+        cs = json.load(open(paths[-1]))["counters"]
+        c = cs[next(k for k in cs if "raster_kernel<1" in k)]
         return round(c["SQ_ACTIVE_INST_VALU"] * 4 / (c["GRBM_GUI_ACTIVE"] / 8 * 1024), 4)
-    except (OSError, KeyError, ValueError, ZeroDivisionError):
+    except (OSError, KeyError, ValueError, ZeroDivisionError, StopIteration):
         return None
 
 
@@ -332,7 +333,7 @@ def main():
                        "fitness_gather": (GATHER if distributed else None)},
             "gsplat_pixels_per_s": round(value * N_SPLATS * H * W / 1e9, 2),
             "aabb_pairs_per_s": round(value * pairs_per_cand, 1),
-            "roofline": {"bound": "hbm", "kernel": "raster_kernel<1>",
+            "roofline": {"bound": "hbm", "kernel": "raster_kernel<1, false>",
                          "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
                          "traffic": None if traffic is None else round(traffic),
