@@ -1258,14 +1258,20 @@ int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_
     GaParamsDev prm = ga_params(s->cfg, it, total_iters);
     prm.mutate_only = 1;
     prm.o_base = first_try;
-    {   // the neighbours and their raster records (prep fused into the variation kernel)
+    // The neighbours and their raster records.  The variation kernel runs one
+    // workgroup per neighbour; fusing the prep into it pays while that leaves few
+    // splats per thread, but a handful of 4,096-splat neighbours (configs[4]) would
+    // prep 16 splats per thread on a few CUs (99 us): then the prep kernel runs
+    // separately, one thread per splat (same ggs_prep.h math, same bits).
+    const bool fuse_prep = s->N <= 1024 || n >= 64;
+    {
         ProfScope ps(s->st, 0);
         GGS_HIP(launch_ga_variation(s->st, (const float*)s->curr.p, nullptr, 1, s->N, prm, d, s->cfg.seed, it,
-                                    (float*)s->nb.p, n, (SplatRec*)s->nb_recs.p, s->cfg.H, s->cfg.W,
-                                    s->cfg.k_sigma));
+                                    (float*)s->nb.p, n, fuse_prep ? (SplatRec*)s->nb_recs.p : nullptr,
+                                    s->cfg.H, s->cfg.W, s->cfg.k_sigma));
     }
     if ((rc = sa_eval(s, (const float*)s->nb.p, n, (SplatRec*)s->nb_recs.p, (float*)s->nb_part.p,
-                      (float*)s->nb_fits.p, s->incremental, true)))
+                      (float*)s->nb_fits.p, s->incremental, fuse_prep)))
         return rc;
     GGS_HIP(hipMemcpyAsync(s->h_fits, s->nb_fits.p, sizeof(float) * n, hipMemcpyDeviceToHost, s->st));
     GGS_HIP(hipMemcpyAsync(s->h_counters, s->counters.p, sizeof(unsigned), hipMemcpyDeviceToHost, s->st));

@@ -92,8 +92,12 @@ __device__ int tournament_pick(const float* __restrict__ fits, const GaDrawsDev&
     return best;
 }
 
-constexpr int VT = 256;   // threads per variation workgroup
-
+// Threads per variation workgroup (one workgroup per offspring): 256 for a GA
+// generation (P workgroups fill the chip); 1024 when a few large offspring are
+// bred (SA tries at configs[4]: 4,096 splats each), which otherwise leave 16
+// splats per thread on a handful of CUs.  Results do not depend on VT (per-splat
+// work, an OR, a sum and an in-order search).
+template <int VT>
 __global__ void __launch_bounds__(VT)
 ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fits, int P, int N,
                     GaParamsDev prm, GaDrawsDev d, uint32_t k0, uint32_t k1, int gen,
@@ -479,8 +483,12 @@ ga_gather_kernel(const float* __restrict__ pop, const float* __restrict__ off, i
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
                                float* off, int n_off, SplatRec* recs, int H, int W, float k_sigma) {
-    hipLaunchKernelGGL(ga_variation_kernel, dim3(n_off), dim3(VT), 0, st, pop, fits, P, N, prm, d,
-                       (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma);
+    if (n_off < 64 && N >= 1024)
+        hipLaunchKernelGGL(ga_variation_kernel<1024>, dim3(n_off), dim3(1024), 0, st, pop, fits, P, N, prm, d,
+                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma);
+    else
+        hipLaunchKernelGGL(ga_variation_kernel<256>, dim3(n_off), dim3(256), 0, st, pop, fits, P, N, prm, d,
+                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma);
     return hipGetLastError();
 }
 

@@ -108,7 +108,17 @@ __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
 __device__ __forceinline__ double wave_sum(const float* __restrict__ x, int n) {
     const int lane = threadIdx.x & 63;
     double a = 0.0;
-    for (int i = lane; i < n; i += 64) a += (double)x[i];
+    int i = lane;
+    // eight loads in flight, then the same in-order adds (2,048 strip partials at
+    // 2048^2 were 32 dependent HBM round trips per lane: 16 us per finalize)
+    for (; i + 7 * 64 < n; i += 8 * 64) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = x[i + k * 64];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a += (double)v[k];
+    }
+    for (; i < n; i += 64) a += (double)x[i];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
     return a;

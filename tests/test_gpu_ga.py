@@ -161,7 +161,10 @@ def _sa(target, H, W, N, **kw):
 @pytest.mark.parametrize("H,W,N,tries,boost,spec", [(40, 40, 17, 4, False, None),
                                                      (64, 48, 300, 3, True, 1),
                                                      (32, 32, 1, 5, False, 5),
-                                                     (48, 48, 2, 8, False, None)])
+                                                     (48, 48, 2, 8, False, None),
+                                                     # >= 1024 splats: 1024-thread variation
+                                                     # workgroups, prep unfused, N > 512 raster
+                                                     (64, 64, 1100, 3, False, None)])
 def test_device_sa_matches_host_sa_with_same_draws(H, W, N, tries, boost, spec):
     target, _, _ = _problem(H, W, 5)
     init = ga.new_population(1, N, H, W, MIN_S, MAX_S, np.random.default_rng(N))[0]
