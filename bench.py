@@ -89,12 +89,21 @@ def synthetic_population(B, N, seed):
     return G
 
 
+def _bench_profiles():
+    """profiles/rNN/summary.json of this workload, oldest round first (the
+    profiles/rNN_<config> directories hold the other configs)."""
+    import glob
+    import re
+    return sorted(p for p in glob.glob(os.path.join(REPO, "profiles", "r*", "summary.json"))
+                  if re.fullmatch(r"r\d+", os.path.basename(os.path.dirname(p))))
+
+
 def pmc_traffic():
     """HBM bytes per raster launch from the newest committed rocprofv3 PMC
     summary of this same workload (tools/profile.sh -> profiles/rNN/summary.json:
     FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE); None when absent."""
     import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "summary.json")))
+    paths = _bench_profiles()
     if not paths:
         return None, None
     try:
@@ -109,7 +118,7 @@ def pmc_valu_busy():
     committed PMC summary: SQ_ACTIVE_INST_VALU (quad-cycles, summed over SIMDs)
     x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); None when absent."""
     import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "summary.json")))
+    paths = _bench_profiles()
     if not paths:
         return None
     try:
