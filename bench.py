@@ -178,6 +178,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="512")
+    ap.add_argument("--ramp-ms", type=float, default=300.0,
+                    help="untimed steps before the warm-up, until the clocks have ramped")
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="HIP streams the independent batches alternate over (1 = dependent batches)")
     args = ap.parse_args()
@@ -247,11 +249,11 @@ def main():
             works[j].wait()
         works[j] = None
 
-    def step(i, ns):
+    def step(i, ns, gather=True):
         g, j, st = pops[i % N_POPS], i % RING, sts[i % ns]
         join(j)
         plan.fitness_device(st, g.data_ptr(), POP, N_SPLATS, 9, K_SIGMA, outs[j].data_ptr())
-        if not distributed or GATHER == "none":
+        if not distributed or GATHER == "none" or not gather:
             return
         if comm is not None:                                 # RCCL: fitness scalars to every rank
             works[j] = (i % ns, comms[i % ns].allgather(st, outs[j].data_ptr(), gathered[j].data_ptr(), POP,
@@ -268,6 +270,22 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    # Clock ramp before any measurement: the GPU raises its clocks over tens of ms
+    # of load (a 30-step run right after set-up measured the raster at 0.187-0.195
+    # ms vs 0.178 ms in steady state), so run the evaluation untimed for --ramp-ms
+    # first (no gathers: ranks may run different numbers of these steps).
+    def ramp(ms, ns):
+        t_ramp, i = time.perf_counter(), 0
+        while (time.perf_counter() - t_ramp) * 1e3 < ms:
+            for _ in range(50):
+                step(i, ns, gather=False)
+                i += 1
+            torch.cuda.synchronize(dev)
+        barrier()
+
+    barrier()                  # first collective's one-time set-up before the ramp, not after it
+    ramp(args.ramp_ms, args.streams)
+
     def timed(ns):
         """W untimed + K timed steps over ns streams: (max-over-ranks seconds, host enqueue s)."""
         for i in range(args.warmup):
@@ -278,32 +296,45 @@ def main():
             step(i, ns)
         host_s = time.perf_counter() - t0                   # enqueue time (host side)
         barrier()
-        el = time.perf_counter() - t0
-        if distributed:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el, host_s
+        return time.perf_counter() - t0, host_s
 
     elapsed, host_s = timed(args.streams)                  # the headline
     if distributed and GATHER != "none":                    # the gather delivered this rank's shard
         j = (args.steps - 1) % RING
-        mine = gathered[j][rank * POP:(rank + 1) * POP]
-        assert torch.equal(mine, outs[j]), "fitness all-gather returned a different shard"
+        shard_ok = torch.equal(gathered[j][rank * POP:(rank + 1) * POP], outs[j])
     # dependent batches (a GA generation needs the previous one's fitness): one stream
-    elapsed1, _ = timed(1) if args.streams > 1 else (elapsed, host_s)
+    # (each later pass gets a short ramp too: under torchrun the first passes after
+    # a switch measured 5-15 % slow, tools/probe/pass_speed.py)
+    if args.streams > 1:
+        ramp(args.ramp_ms / 3, 1)
+        elapsed1, _ = timed(1)
+    else:
+        elapsed1 = elapsed
+    ramp(args.ramp_ms / 3, 1)
 
     # per-kernel device time (HIP events on the launch stream) over a third,
     # single-stream pass (kernels alone, not sharing the chip with the other
     # stream's): the raster kernel is the dominant one
-    ggs.profile_reset()
-    ggs.profile_enable(True)
-    for i in range(args.steps):
-        step(i, 1)
-    barrier()
-    ggs.profile_enable(False)
+    for rep in range(int(os.environ.get("GGS_BENCH_PROFILE_REPS", "1"))):
+        ggs.profile_reset()
+        ggs.profile_enable(True)
+        for i in range(args.steps):
+            step(i, 1)
+        barrier()
+        ggs.profile_enable(False)
+        if os.environ.get("GGS_BENCH_PROFILE_REPS") and rank == 0:
+            ms_, n_ = ggs.profile_read("raster")
+            print(f"profile pass {rep}: raster {ms_ / max(n_, 1):.4f} ms", file=sys.stderr, flush=True)
     kern = {k: ggs.profile_read(k) for k in ("prep", "raster", "finalize")}
     raster_ms = kern["raster"][0] / max(kern["raster"][1], 1)
+    # max over ranks, after every measured pass (a first all-reduce between the
+    # passes idles the GPU long enough for the clocks to drop)
+    if distributed:
+        t = torch.tensor([elapsed, elapsed1], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, elapsed1 = (float(v) for v in t.tolist())
+        if GATHER != "none":
+            assert shard_ok, "fitness all-gather returned a different shard"
 
     # algorithmic work of this workload (AABB pairs from the product's own prep)
     pairs = 0
