@@ -185,6 +185,38 @@ def test_render_saturation_cutoff_within_2pow24(H, W):
     np.testing.assert_allclose(img, O.render(G, H, W), atol=1e-5, rtol=0)
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_render_and_fitness_fuzz_vs_oracle(seed):
+    """Seeded random shapes and populations: canvas 1..300 per side (strips and
+    tiles cut by the image edge), 1..1,500 splats (past the 512-splat cut-off
+    threshold and the 1,024-entry strip list), raw genome values well outside
+    the reference's ranges, k_sigma 1..4, random background; images within the
+    1e-4 bar, fitness within 1e-5 relative (weighted / plain / boost modes)."""
+    rng = np.random.default_rng(1000 + seed)
+    H, W = int(rng.integers(1, 301)), int(rng.integers(1, 301))
+    B, N = int(rng.integers(1, 4)), int(rng.choice([1, 7, 64, 300, 700, 1500]))
+    G = np.empty((B, N, 9), np.float32)
+    G[..., 0:2] = rng.uniform(-0.2, 1.2, (B, N, 2))
+    G[..., 2:4] = rng.uniform(-1.0, np.log(0.15 * max(H, W)) + 1.0, (B, N, 2))
+    G[..., 4] = rng.uniform(-8, 8, (B, N))
+    G[..., 5:9] = rng.uniform(-40, 300, (B, N, 4))
+    k = float(rng.uniform(1.0, 4.0))
+    bg = tuple(float(v) for v in rng.uniform(0, 1, 3))
+    img = ggs.render(G, H, W, k_sigma=k, background=bg)
+    np.testing.assert_allclose(img, O.render(G, H, W, k_sigma=k, background=bg), atol=IMG_TOL, rtol=0)
+    A = np.empty((B, N, 9), np.float32)                     # axes-angle genomes for fitness
+    A[..., 0:2] = rng.uniform(0, 1, (B, N, 2))
+    A[..., 2:4] = rng.uniform(np.log(1.0), np.log(0.1 * max(H, W) + 2), (B, N, 2))
+    A[..., 4] = rng.uniform(-np.pi, np.pi, (B, N))
+    A[..., 5:9] = rng.uniform(0, 255, (B, N, 4))
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0, 1, (H, W)).astype(np.float32)
+    for m, boost in ((mask, False), (None, False), (mask, True)):
+        got = ggs.fitness(A, tgt, H, W, k, weight_mask=m, boost_only=boost)
+        ref = O.fitness_many(list(A), tgt, H, W, k, weight_mask=m, boost_only=boost)
+        np.testing.assert_allclose(got, ref, rtol=FIT_RTOL)
+
+
 def test_render_edge_inputs():
     H, W = 40, 50
     assert ggs.render(np.zeros((0, 3, 9), np.float32), H, W).shape == (0, H, W, 3)
