@@ -287,7 +287,9 @@ def main():
     ramp(args.ramp_ms, args.streams)
 
     def timed(ns):
-        """W untimed + K timed steps over ns streams: (max-over-ranks seconds, host enqueue s)."""
+        """W untimed + K timed steps over ns streams, bracketed by barrier + synchronize:
+        (this rank's seconds, host enqueue seconds); the max over ranks is taken
+        once every pass has run."""
         for i in range(args.warmup):
             step(i, ns)
         barrier()
