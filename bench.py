@@ -182,10 +182,15 @@ def main():
                     help="untimed steps before the warm-up, until the clocks have ramped")
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="HIP streams the independent batches alternate over (1 = dependent batches)")
+    ap.add_argument("--pop", type=int, default=0,
+                    help="candidates per GPU per batch (0: the config's; other values explore batch size "
+                         "and are not the BASELINE workload)")
     args = ap.parse_args()
     global H, W, N_SPLATS, POP
     H, N_SPLATS, POP = CONFIGS[args.config]
     W = H
+    if args.pop > 0:
+        POP = args.pop
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -364,11 +369,11 @@ def main():
     raster_bytes = bytes_per_candidate() * POP
     achieved_gbs = raster_bytes / (raster_ms * 1e-3) / 1e9
     valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic() if args.config == "512" else (None, None)
+    traffic, traffic_src = pmc_traffic() if args.config == "512" and POP == 128 else (None, None)
     if rank == 0:
         line = {
             "metric": "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=128"
-                      if args.config == "512" else
+                      if args.config == "512" and POP == 128 else
                       f"candidate renders/sec, {H}x{W}, {N_SPLATS} splats, pop={POP} per GPU",
             "value": round(value, 1),
             "unit": "candidate renders/s",
@@ -401,7 +406,7 @@ def main():
                      "flop_per_aabb_pair": FLOP_PER_PAIR, "aabb_pairs_per_candidate": pairs_per_cand,
                      "accounting": "reference-equivalent work: 24 FLOP per AABB pair (SURVEY.md §8d); "
                                    "the row recurrence executes fewer, so frac can exceed 1",
-                     "busy_pmc": pmc_valu_busy() if args.config == "512" else None},
+                     "busy_pmc": pmc_valu_busy() if args.config == "512" and POP == 128 else None},
             "streams": args.streams,
             "value_one_stream": round(world * POP * args.steps / elapsed1, 1),
             "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4),
