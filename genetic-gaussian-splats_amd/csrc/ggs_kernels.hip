@@ -95,6 +95,9 @@ constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull
 #ifndef GGS_XCD_SPREAD
 #define GGS_XCD_SPREAD 1          // spread each candidate's strips over the XCDs
 #endif
+#ifndef GGS_PK_EPI
+#define GGS_PK_EPI 1              // fitness epilogue colours by v_pk_fma_f32 ... clamp (inline asm;
+#endif                            // bit-identical to the scalar v_fma clamp path, ~1 % faster)
 #ifndef GGS_CULL_PF
 #define GGS_CULL_PF 1             // cull bounds loads in flight (chunks of 64 splats)
 #endif
@@ -635,9 +638,24 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         // lines up with the packed accumulators (two pixels per v_pk op).
         const float4* __restrict__ P = plan + (int64_t)(t * 4 + wv) * RG * 64 + lane;
         f2_t accp = 0.0f;
+#if GGS_PK_EPI
+        // background pairs (bg, bg) in SGPR pairs: no VGPRs at the epilogue's peak
+        const uint64_t bg2r = (uint64_t)__float_as_uint(bg_r) * 0x100000001ull;
+        const uint64_t bg2g = (uint64_t)__float_as_uint(bg_g) * 0x100000001ull;
+        const uint64_t bg2b = (uint64_t)__float_as_uint(bg_b) * 0x100000001ull;
+#endif
 #pragma unroll
         for (int k = 0; k < NPK; ++k) {
             const float4 qa = P[(2 * k) * 64], qb = P[(2 * k + 1) * 64];
+#if GGS_PK_EPI
+            // packed: one v_pk_fma_f32 with the clamp bit per channel and row pair
+            // (the compiler folds the clamp only into the scalar v_fma_f32)
+            const f2_t T2 = {T[2 * k], T[2 * k + 1]};
+            f2_t c_r, c_g, c_b;
+            asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(c_r) : "v"(T2), "s"(bg2r), "v"((f2_t){R[2 * k], R[2 * k + 1]}));
+            asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(c_g) : "v"(T2), "s"(bg2g), "v"((f2_t){G[2 * k], G[2 * k + 1]}));
+            asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(c_b) : "v"(T2), "s"(bg2b), "v"((f2_t){Bl[2 * k], Bl[2 * k + 1]}));
+#else
             f2_t c_r, c_g, c_b;       // clamp folds into the scalar v_fma (clamp bit)
             c_r.x = fminf(fmaxf(__builtin_fmaf(T[2 * k], bg_r, R[2 * k]), 0.0f), 1.0f);
             c_r.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_r, R[2 * k + 1]), 0.0f), 1.0f);
@@ -645,6 +663,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             c_g.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_g, G[2 * k + 1]), 0.0f), 1.0f);
             c_b.x = fminf(fmaxf(__builtin_fmaf(T[2 * k], bg_b, Bl[2 * k]), 0.0f), 1.0f);
             c_b.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_b, Bl[2 * k + 1]), 0.0f), 1.0f);
+#endif
             const f2_t dr = c_r - (f2_t){qa.x, qa.y};
             const f2_t dg = c_g - (f2_t){qa.z, qa.w};
             const f2_t db = c_b - (f2_t){qb.x, qb.y};
