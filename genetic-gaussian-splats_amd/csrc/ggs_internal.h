@@ -13,10 +13,12 @@ namespace ggs {
 // r, g, b: colour in [0,1] (render.py:40-42); x0..y1: inclusive integer AABB
 // (render.py:27-30).
 struct __attribute__((aligned(16))) SplatRec {
-    float cx, cy, A, Bc;
-    float Cc, la, r, g;
-    float b;
-    float rho, c16, rho4;  // row-recurrence constants: 2^(128 Cc), 16 Cc, 2^(64 Cc) (8-row step)
+    // Cc, r, g, b, rho sit in odd dwords: the raster broadcasts them to both halves
+    // of its v_pk_* ops straight from the record's SGPR pair (op_sel hi) instead of
+    // copying each into a pair of its own per visit.
+    float cx, Cc, cy, r;
+    float A, g, Bc, b;
+    float la, rho, c16, rho4;  // row-recurrence constants: 2^(128 Cc), 16 Cc, 2^(64 Cc) (8-row step)
     int x0, x1, y0, y1;
 };
 static_assert(sizeof(SplatRec) == 64, "SplatRec must be 64 bytes");

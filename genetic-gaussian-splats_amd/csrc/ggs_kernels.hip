@@ -204,7 +204,7 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
     do {                                                                             \
         if (GGS_ABL == 2) break;                                                     \
         const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                   \
-        f2_t e_ = fma2(qy_, fma2(Cc2, qy_, bx2), px2);                               \
+        f2_t e_ = fma2(qy_, fma2((f2_t)s.Cc, qy_, bx2), px2);                               \
         if (MASKED) {                                                                \
             if ((unsigned)(8 * (k) - rlo) > rspan) e_.x = -__builtin_inff();         \
             if ((unsigned)(8 * (k) + 4 - rlo) > rspan) e_.y = -__builtin_inff();     \
@@ -213,9 +213,9 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
         f_.x = GGS_EXP2(e_.x);                                                       \
         f_.y = GGS_EXP2(e_.y);                                                       \
         const f2_t w_ = P_T##k * f_;                                                 \
-        P_R##k = fma2(w_, cr2, P_R##k);                                              \
-        if (GGS_ABL != 3) P_G##k = fma2(w_, cg2, P_G##k);                            \
-        if (GGS_ABL != 3) P_B##k = fma2(w_, cb2, P_B##k);                            \
+        P_R##k = fma2((f2_t)s.r, w_, P_R##k);                                              \
+        if (GGS_ABL != 3) P_G##k = fma2((f2_t)s.g, w_, P_G##k);                            \
+        if (GGS_ABL != 3) P_B##k = fma2((f2_t)s.b, w_, P_B##k);                            \
         P_T##k = P_T##k - w_;                                                        \
     } while (0)
 // Blend one packed pair with given (row-masked) Gaussian values f.
@@ -223,9 +223,9 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
     do {                                                                             \
         if (GGS_ABL == 2) break;                                                     \
         const f2_t w_ = P_T##k * (F);                                                \
-        P_R##k = fma2(w_, cr2, P_R##k);                                              \
-        if (GGS_ABL != 3) P_G##k = fma2(w_, cg2, P_G##k);                            \
-        if (GGS_ABL != 3) P_B##k = fma2(w_, cb2, P_B##k);                            \
+        P_R##k = fma2((f2_t)s.r, w_, P_R##k);                                              \
+        if (GGS_ABL != 3) P_G##k = fma2((f2_t)s.g, w_, P_G##k);                            \
+        if (GGS_ABL != 3) P_B##k = fma2((f2_t)s.b, w_, P_B##k);                            \
         P_T##k = P_T##k - w_;                                                        \
     } while (0)
 #define GGS_BLEND_REC(k)                                                             \
@@ -360,7 +360,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             const int dy0 = y0 - ty0, dy1 = y1 - ty0;          // AABB rows relative to the tile
             const int gA = max(dy0, 0) >> 2;                   // first / last row group
             const int gB = min(dy1, TILE_H - 1) >> 2;
-            const float Cc = s.Cc, cr = s.r, cg = s.g, cb = s.b;
+            [[maybe_unused]] const float Cc = s.Cc, cr = s.r, cg = s.g, cb = s.b;   // unpacked walk
             const float qx = Xf - s.cx;
             const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
             const float px = inx ? __builtin_fmaf(s.A * qx, qx, s.la) : -__builtin_inff();
@@ -370,8 +370,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             const unsigned rspan = (unsigned)(y1 - y0);
 
 #if GGS_PACKED
-            const f2_t qyv = {qy0, qy0 + 4.0f}, Cc2 = Cc, bx2 = bx, px2 = px;
-            const f2_t cr2 = cr, cg2 = cg, cb2 = cb;
+            const f2_t qyv = {qy0, qy0 + 4.0f}, bx2 = bx, px2 = px;
             const int kA = gA >> 1, kB = gB >> 1;             // first / last group pair
             f2_t F2, R2;                                       // row recurrence: f, ratio
             // First pair: exact exponent; keeps the unmasked f as the recurrence
@@ -384,7 +383,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             // test: one straight-line block, the same arithmetic as the general
             // walk (kA = 0, kB = NPK-1, all-ones masks), so the same bits.
             if (max(dy0, TILE_H - 1 - dy1) <= 0) {            // y0 <= ty0 and y1 >= ty0 + 127
-                const f2_t e_ = fma2(qyv, fma2(Cc2, qyv, bx2), px2);
+                const f2_t e_ = fma2(qyv, fma2((f2_t)s.Cc, qyv, bx2), px2);
                 F2.x = GGS_EXP2(e_.x);
                 F2.y = GGS_EXP2(e_.y);
                 if (__ballot((px > -__builtin_inff()) &
@@ -413,7 +412,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     case k:                                                                             \
         if (k < NPK) {                                                                  \
             const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                  \
-            const f2_t e_ = fma2(qy_, fma2(Cc2, qy_, bx2), px2);                        \
+            const f2_t e_ = fma2(qy_, fma2((f2_t)s.Cc, qy_, bx2), px2);                        \
             F2.x = GGS_EXP2(e_.x);                                                      \
             F2.y = GGS_EXP2(e_.y);                                                      \
             f2_t fu_;                                                                   \
