@@ -273,7 +273,14 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     // candidates rotate by one per group: with B % 8 == 0 a fixed b would stay on
     // one XCD (blocks go round-robin to the 8 XCDs) and per-XCD work would be the
     // sum of 16 candidates' costs (tools/probe/wave_timing.py: XCD end times 197-207 us)
-    const int b = (int)((blockIdx.x + gi) % B);
+    // ... but only every 2^GGS_XCD_SHIFT groups: blocks B apart (the next group's
+    // block in the same XCD slot) then run the same candidate, whose records stay
+    // in that XCD's caches across 8 groups (raster -0.5 %, one stream +0.7 %;
+    // shifts 2-5 measured alike, 0 = rotate every group)
+#ifndef GGS_XCD_SHIFT
+#define GGS_XCD_SHIFT 3
+#endif
+    const int b = (int)((blockIdx.x + (gi >> GGS_XCD_SHIFT)) % B);
 #else
     const int b = blockIdx.x % B;
 #endif
