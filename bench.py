@@ -9,7 +9,7 @@ weighted L2 + finalize (libggs.so, device-pointer API, inputs resident in HBM),
 plus — for N > 1 GPUs — the RCCL all-gather of the fitness scalars (libggs
 ggs_comm_allgather on the compute stream; the only exchange step; candidates
 are sharded, weak scaling).  Consecutive populations are independent and
-alternate over --streams HIP streams (default 2); `value_one_stream` is the rate
+alternate over --streams HIP streams (default 4); `value_one_stream` is the rate
 when each step must wait for the previous one (a GA generation).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S] [--config 512|1024]
@@ -41,7 +41,7 @@ N_SPLATS = 256
 POP = 128
 K_SIGMA = 3.0
 N_POPS = 4
-RING = 4                         # in-flight fitness vectors (gather overlap)
+RING = 8                         # in-flight fitness vectors (gather overlap)
 # How the per-batch fitness all-gather is issued (A/B switch, tools/gather_exp.sh;
 # "none" is a diagnostic, not a valid N>1 configuration):
 #   "rccl"         (default) libggs's RCCL communicator, in order on the compute
@@ -51,12 +51,15 @@ RING = 4                         # in-flight fitness vectors (gather overlap)
 #   "torch" / "torch-sync"  torch.distributed all_gather_into_tensor, async through
 #                  the ring / waited: +11 / +24 us
 GATHER = os.environ.get("GGS_BENCH_GATHER", "rccl")
-# Consecutive batches are independent populations, so they alternate over two
-# HIP streams: one batch's raster fills the CUs the other's grid tail (and its
+# Consecutive batches are independent populations, so they alternate over four
+# HIP streams: one batch's raster fills the CUs the others' grid tails (and their
 # prep/finalize launches) leave idle — tools/streams_exp.sh: 0.189 -> 0.173 ms
-# per batch.  A GA generation depends on the previous one's fitness and runs at
-# the one-stream rate, reported beside as value_one_stream.
-STREAMS = int(os.environ.get("GGS_BENCH_STREAMS", "2"))
+# per batch at two streams; four add 2 % more (tools/probe/streams_ab.sh,
+# streams_tr.sh: 781-786k vs 766-768k renders/s, the same under torchrun;
+# eight streams 763-768k, 16 hardware queues instead of 8 no different).
+# A GA generation depends on the previous one's fitness and runs at the
+# one-stream rate, reported beside as value_one_stream.
+STREAMS = int(os.environ.get("GGS_BENCH_STREAMS", "4"))
 # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); under
 # torchrun torch's and RCCL's streams take queues too and the second compute
 # stream ends up sharing one (669k vs 730k renders/s at world 1), so ask for 8.
