@@ -329,11 +329,14 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 #if GGS_CULL_PF >= 4
     int4 bbn3 = bounds(N - 1 - 128 - lane), bbn4 = bounds(N - 1 - 192 - lane);
 #endif
+#ifndef GGS_CULL_PRIO
+#define GGS_CULL_PRIO 2              // 1 and 3 measured the same
+#endif
 #ifndef GGS_PRIO
 #define GGS_PRIO 1          // wave priority: culls (load-bound) ahead of blends; +0.4 %
 #endif
     for (int base = 0; base < N; base += 64) {
-        if (GGS_PRIO == 1) __builtin_amdgcn_s_setprio(2);   // cull: loads issue first
+        if (GGS_PRIO == 1) __builtin_amdgcn_s_setprio(GGS_CULL_PRIO);   // cull: loads issue first
         // --- cull 64 splats (descending index = front-to-back) against the strip:
         // one 16-B load per lane (clamped index, no short-circuit: a branchy test
         // splits it into two dependent loads), then a branch-free overlap test
