@@ -3,27 +3,49 @@
 
 Workload (BASELINE.json `metric`, configs[1]): 512x512 canvas, 256 splats per
 candidate, pop = 128 candidates per GPU, weighted-L2 fitness (the GA's default
-path, fitness.py:28-31 with the importance mask) — one *step* = the evaluation
-of one population of 128 candidates per GPU: encode + preprocess + raster + fused
-weighted L2 + finalize (libggs.so, device-pointer API, inputs resident in HBM),
-plus — for N > 1 GPUs — the RCCL all-gather of the fitness scalars (libggs
-ggs_comm_allgather on the compute stream; the only exchange step; candidates
-are sharded, weak scaling).  Consecutive populations are independent and
-alternate over --streams HIP streams (default 4); `value_one_stream` is the rate
-when each step must wait for the previous one (a GA generation).
+path, fitness.py:28-31 with the importance mask).  One *step* = the evaluation
+of one population: encode + preprocess + raster + fused weighted L2 + finalize
+(libggs.so, device-pointer API, inputs resident in HBM) and — on more than one
+GPU — the RCCL all-gather of the fitness scalars (libggs ggs_comm_allgather on
+the compute stream; the only exchange step).  Consecutive populations are
+independent and alternate over --streams HIP streams (default 4);
+`value_one_stream` is the rate when each step must wait for the previous one (a
+GA generation), `value_with_readback` adds the per-step D2H of the B fitness
+scalars (fitness.py:42 `.cpu()`).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S] [--config 512|1024]
+No PyTorch anywhere (north_star): device memory and streams come from ggs.hip
+(ctypes over the HIP runtime libggs uses), the collectives from libggs's own RCCL
+communicators, their id from a file rendezvous on the node.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S]
+                    [--config 512|1024|1024x8]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line.  Synthetic data: genomes drawn from the
-population.py:20-46 distributions (4 different populations resident in HBM,
-cycled step to step), target U[0,1], mask U[0.405,1].
+`--gpus N` outside a launcher starts N rank processes itself (before anything
+touches a GPU) with RANK / LOCAL_RANK / WORLD_SIZE set, exactly what torchrun
+would; under a launcher WORLD_SIZE must equal N.  Rank 0 prints ONE JSON line.
+
+Configs: "512" (default; configs[1], weak scaling: 128 candidates per GPU),
+"1024" (configs[2]: 1024^2 / 1024 splats / 512 per GPU, weak) and "1024x8"
+(configs[3]: 1024^2 / 1024 splats, ONE population of 4096 split over the N GPUs,
+strong scaling).  Synthetic data: genomes from the population.py:20-46
+distributions (4 populations resident in HBM, cycled step to step), target
+U[0,1], mask U[0.405,1].
+
+Timing: W untimed steps, then passes of exactly K steps, each bracketed by a
+barrier + device synchronize on both sides; passes repeat until >= --min-time
+seconds were measured (the driver's --steps 20 is ~3 ms, inside launch/clock
+jitter); the reported time is the median pass, after taking the max over ranks
+pass by pass.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,40 +54,29 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "genetic-gaussian-splats_amd"))
 
-# BASELINE.json configs: [1] is the metric's workload (default); [2] is the
-# 1024^2 / 1024-splat / pop-512 single-GPU case (--config 1024), whose per-GPU
-# shard is also configs[3] (pop 4096 over 8 GPUs = 512 per GPU).
-CONFIGS = {"512": (512, 256, 128), "1024": (1024, 1024, 512)}
+# name -> (H = W, splats, candidates, scaling).  "1024x8": the candidates are the
+# GLOBAL population, split over the ranks (strong scaling); otherwise per GPU.
+CONFIGS = {"512": (512, 256, 128, "weak"), "1024": (1024, 1024, 512, "weak"),
+           "1024x8": (1024, 1024, 4096, "strong")}
 H = W = 512
 N_SPLATS = 256
 POP = 128
 K_SIGMA = 3.0
 N_POPS = 4
 RING = 8                         # in-flight fitness vectors (gather overlap)
-# How the per-batch fitness all-gather is issued (A/B switch, tools/gather_exp.sh;
-# "none" is a diagnostic, not a valid N>1 configuration):
-#   "rccl"         (default) libggs's RCCL communicator, in order on the compute
-#                  stream right after finalize: +1.5 us per step at world 1
-#   "rccl-overlap" the same on the communicator's own stream, joined through the
-#                  ring: +21 us (the cross-stream event waits cost more than they hide)
-#   "torch" / "torch-sync"  torch.distributed all_gather_into_tensor, async through
-#                  the ring / waited: +11 / +24 us
+METRIC = "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=128"
+# How the per-step fitness all-gather is issued (A/B switch, tools/gather_exp.sh):
+#   "rccl"          (default) libggs's RCCL communicator, in order on the compute
+#                   stream right after finalize: +1.5 us per step at world 1
+#   "rccl-overlap"  the same on the communicator's own stream, joined through the
+#                   ring: +21 us (the cross-stream event waits cost more than they hide)
+#   "none"          diagnostic only, not a valid N > 1 configuration
 GATHER = os.environ.get("GGS_BENCH_GATHER", "rccl")
 # Consecutive batches are independent populations, so they alternate over four
 # HIP streams: one batch's raster fills the CUs the others' grid tails (and their
-# prep/finalize launches) leave idle — tools/streams_exp.sh: 0.189 -> 0.173 ms
-# per batch at two streams; four add 2 % more (tools/probe/streams_ab.sh,
-# streams_tr.sh: 781-786k vs 766-768k renders/s, the same under torchrun;
-# eight streams 763-768k, 16 hardware queues instead of 8 no different).
-# A GA generation depends on the previous one's fitness and runs at the
-# one-stream rate, reported beside as value_one_stream.
+# prep/finalize launches) leave idle (781-786k vs 766-768k
+# renders/s at two streams, eight 763-768k).
 STREAMS = int(os.environ.get("GGS_BENCH_STREAMS", "4"))
-# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); under
-# torchrun torch's and RCCL's streams take queues too and the second compute
-# stream ends up sharing one (669k vs 730k renders/s at world 1), so ask for 8.
-# Read by the HIP runtime at initialisation, which happens after this line.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md: peak FP32 vector
 FLOP_PER_PAIR = 24
@@ -101,18 +112,24 @@ def _bench_profiles():
                   if re.fullmatch(r"r\d+", os.path.basename(os.path.dirname(p))))
 
 
-def pmc_traffic():
-    """HBM bytes per raster launch from the newest committed rocprofv3 PMC
-    summary of this same workload (tools/profile.sh -> profiles/rNN/summary.json:
-    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE); None when absent."""
-    import glob
+def _summary():
     paths = _bench_profiles()
     if not paths:
         return None, None
     try:
-        d = json.load(open(paths[-1]))
-        return d["raster_hbm_bytes_per_launch"]["total"], os.path.relpath(paths[-1], REPO)
-    except (OSError, KeyError, ValueError):
+        return json.load(open(paths[-1])), os.path.relpath(paths[-1], REPO)
+    except (OSError, ValueError):
+        return None, None
+
+
+def pmc_traffic():
+    """HBM bytes per raster launch from the newest committed rocprofv3 PMC
+    summary of this same workload (tools/profile.sh -> profiles/rNN/summary.json:
+    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE); None when absent."""
+    d, src = _summary()
+    try:
+        return d["raster_hbm_bytes_per_launch"]["total"], src
+    except (TypeError, KeyError):
         return None, None
 
 
@@ -120,18 +137,27 @@ def pmc_valu_busy():
     """Fraction of SIMD cycles the raster kernel's VALU was busy, from the same
     committed PMC summary: SQ_ACTIVE_INST_VALU (quad-cycles, summed over SIMDs)
     x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); None when absent."""
-    import glob
-    paths = _bench_profiles()
-    if not paths:
-        return None
+    d, _ = _summary()
     try:
-        cs = json.load(open(paths[-1]))["counters"]
+        cs = d["counters"]
         c = cs[next(k for k in cs if "raster_kernel<1" in k)]
         return round(c["SQ_ACTIVE_INST_VALU"] * 4 / (c["GRBM_GUI_ACTIVE"] / 8 * 1024), 4)
-    except (OSError, KeyError, ValueError, ZeroDivisionError, StopIteration):
+    except (TypeError, KeyError, ZeroDivisionError, StopIteration):
         return None
 
 
+def pmc_trace_avg_us():
+    """The committed rocprofv3 kernel-trace average of the raster kernel over a
+    single-stream bench pass (tools/profile.sh runs bench.py --streams 1)."""
+    d, _ = _summary()
+    try:
+        return d.get("raster_profile_pass_avg_us") or \
+            next(v["avg_us"] for k, v in d["kernels"].items() if "raster_kernel<1" in k)
+    except (AttributeError, StopIteration, KeyError):
+        return None
+
+
+# ---- CPU baseline -----------------------------------------------------------------
 def _cpu_worker(args):
     pop, tgt, mask = args
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -139,13 +165,27 @@ def _cpu_worker(args):
     return O.fitness_many(list(pop), tgt, H, W, K_SIGMA, weight_mask=mask)
 
 
+def cpu_cores():
+    """The host cores this job may use: the CPU affinity set, capped by the
+    box's per-job thread budget (OMP_NUM_THREADS; the GPU box grants 16 of its
+    256 CPUs to a one-GPU job, so os.cpu_count() overstates what runs)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
 def cpu_baseline(tgt, mask, per_worker=80):
     """The oracle (numpy restatement of render.py + fitness.py) timed on the
     host cores, candidates split over a process pool (80 per process: a ~10 s
     bounded sample of the same workload).  Runs BEFORE any GPU initialisation
-    (fork)."""
+    (fork).  BASELINE.md's plan: 1 process, and one process per core."""
     import multiprocessing as mp
-    cores = max(1, min(16, os.cpu_count() or 1))
+    cores = cpu_cores()
     pops = [synthetic_population(per_worker, N_SPLATS, 1000 + i) for i in range(cores)]
     ctx = mp.get_context("fork")
     with ctx.Pool(cores) as pool:
@@ -155,13 +195,16 @@ def cpu_baseline(tgt, mask, per_worker=80):
         dt = time.perf_counter() - t0
     n = cores * per_worker
     t1 = time.perf_counter()                                      # 1 core
-    _cpu_worker((pops[0][:8], tgt, mask))
-    one = 8 / (time.perf_counter() - t1)
-    return {"value": n / dt, "unit": "candidate renders/s", "cores": cores, "kind": "port",
+    _cpu_worker((pops[0][:24], tgt, mask))
+    one = 24 / (time.perf_counter() - t1)
+    return {"value": round(n / dt, 2), "unit": "candidate renders/s", "cores": cores, "kind": "port",
             "sample": f"{n} candidates ({per_worker} per process x {cores} processes, 1 thread each) "
-                      f"at 512x512/256 splats, weighted fitness, oracle/ggs_oracle.py numpy; {dt:.1f} s",
-            "single_core_value": round(one, 2), "cpu_model": _cpu_model(),
-            "host_cpus_visible": os.cpu_count()}
+                      f"at {H}x{W}/{N_SPLATS} splats, weighted fitness, oracle/ggs_oracle.py numpy; "
+                      f"{dt:.1f} s",
+            "single_core_value": round(one, 2), "single_core_sample": "24 candidates, 1 process",
+            "cpu_model": _cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "cores_rule": "CPU affinity set capped by OMP_NUM_THREADS (the job's CPU share on the "
+                          "GPU box; os.cpu_count() counts the whole host)"}
 
 
 def _cpu_model() -> str:
@@ -174,13 +217,77 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def main():
+# ---- rank spawning (--gpus N outside a launcher) ----------------------------------
+def visible_gpus():
+    """GPUs this process could open, counted WITHOUT initialising HIP (the KFD
+    topology: nodes with SIMDs), narrowed by the *_VISIBLE_DEVICES lists; None
+    when unknown."""
+    import glob
+    n = 0
+    try:
+        for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            for line in open(p):
+                if line.startswith("simd_count") and int(line.split()[1]) > 0:
+                    n += 1
+    except (OSError, ValueError):
+        return None
+    if n == 0:
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, python=sys.executable, script=None, gpus_visible=None) -> int:
+    """Run this script as n rank processes (one per GPU) and return the job's
+    exit code: the first failing rank's (the others are then stopped), else 0.
+    The parent never touches a GPU: it only counts the KFD nodes."""
+    have = visible_gpus() if gpus_visible is None else gpus_visible
+    if have is not None and have < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                   GGS_RDZV_KEY=f"bench-{os.getpid()}-{port}")
+        procs.append(subprocess.Popen([python, script or os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:                   # the job failed: stop the other ranks
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---- the benchmark ---------------------------------------------------------------------
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="512")
+    ap.add_argument("--min-time", type=float, default=0.5,
+                    help="repeat the K-step timed pass until this many seconds were measured")
     ap.add_argument("--ramp-ms", type=float, default=300.0,
                     help="untimed steps before the warm-up, until the clocks have ramped")
     ap.add_argument("--streams", type=int, default=STREAMS,
@@ -188,168 +295,200 @@ def main():
     ap.add_argument("--pop", type=int, default=0,
                     help="candidates per GPU per batch (0: the config's; other values explore batch size "
                          "and are not the BASELINE workload)")
-    args = ap.parse_args()
-    global H, W, N_SPLATS, POP
-    H, N_SPLATS, POP = CONFIGS[args.config]
-    W = H
-    if args.pop > 0:
-        POP = args.pop
+    ap.add_argument("--extras", type=int, default=1,
+                    help="0: headline pass only (profiling runs)")
+    return ap.parse_args(argv)
 
+
+def main(argv=None):
+    args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ   # a launcher, even at N=1
+    run(args, world, rank, local_rank, distributed)
+
+
+def run(args, world, rank, local_rank, distributed):
+    global H, W, N_SPLATS, POP
+    H, N_SPLATS, pop_cfg, scaling = CONFIGS[args.config]
+    W = H
+    if scaling == "strong":                      # configs[3]: one population split over the ranks
+        POP = -(-pop_cfg // world)
+        global_batch = pop_cfg
+    else:
+        POP = args.pop if args.pop > 0 else pop_cfg
+        global_batch = POP * world
+    headline = args.config == "512" and POP == 128
 
     rng = np.random.default_rng(1234)
     tgt_h = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
     mask_h = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "512":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and headline and args.extras:
         cpu = cpu_baseline(tgt_h, mask_h)
 
-    import torch
-    import torch.distributed as dist
+    # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the
+    # gathers' RCCL streams take queues too, so ask for 8 before HIP starts
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    os.environ.setdefault("GGS_HIP_RUNTIME", "system")   # no torch in this process: /opt/rocm's HIP
     import ggs
+    from ggs import hip
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ   # torchrun, even at N=1
-    if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+    n_dev = ggs.ensure_init()
+    if local_rank >= n_dev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local_rank} but only {n_dev} GPU(s) visible")
+    hip.set_device(local_rank)
+    ggs.select_devices([local_rank])
 
-    pops = [torch.from_numpy(synthetic_population(POP, N_SPLATS, 10_000 * rank + i)).to(dev)
-            for i in range(N_POPS)]
-    tgt = torch.from_numpy(tgt_h).to(dev)
-    mask = torch.from_numpy(mask_h).to(dev)
-    # fitness vectors in a ring of slots: with an overlapped gather (A/B modes
-    # below) batch i's gather reads outs[i % RING] while batch i+1 is evaluated
-    # into the next slot; a slot is reused only after its gather (device-side wait)
-    outs = [torch.empty(POP, dtype=torch.float32, device=dev) for _ in range(RING)]
-    gathered = [torch.empty(POP * world, dtype=torch.float32, device=dev) for _ in range(RING)]
+    pops_h = [synthetic_population(POP, N_SPLATS, 10_000 * rank + i) for i in range(N_POPS)]
+    pops = [hip.DeviceArray.from_host(p) for p in pops_h]
+    tgt = hip.DeviceArray.from_host(tgt_h)
+    mask = hip.DeviceArray.from_host(mask_h)
+    outs = [hip.DeviceArray((POP,)) for _ in range(RING)]
+    gathered = [hip.DeviceArray((POP * world,)) for _ in range(RING)]
     works = [None] * RING
-    stream = torch.cuda.current_stream(dev)
-    st = stream.cuda_stream
-    # batches alternate over STREAMS HIP streams (independent batches: the next
-    # batch's raster fills the CUs the previous one's grid tail leaves idle)
     assert RING % args.streams == 0, f"--streams must divide {RING}"
-    assert args.streams == 1 or not (distributed and GATHER.startswith("torch")), \
-        "torch.distributed gathers run on torch's current stream: use --streams 1"
-    sts = [st] + [torch.cuda.Stream(dev).cuda_stream for _ in range(args.streams - 1)]
+    streams = [hip.Stream() for _ in range(args.streams)]
+    sts = [s.handle for s in streams]
 
     # the target/mask are fixed over a GA run: lay them out once for the raster's
     # fitness epilogue (ggs_plan_create), as the device-resident GA does
-    plan = ggs.TargetPlan(local_rank, st, tgt.data_ptr(), mask.data_ptr(), ggs.GGS_FIT_WEIGHTED, 1.0,
-                          H, W)
+    plan = ggs.TargetPlan(local_rank, sts[0], tgt.ptr, mask.ptr, ggs.GGS_FIT_WEIGHTED, 1.0, H, W)
+    streams[0].synchronize()
 
     # one RCCL communicator per stream: a communicator orders its collectives
     # across streams, which would serialise the alternating batches again
     comms = [ggs.RcclGather(local_rank) for _ in range(args.streams)] \
         if distributed and GATHER.startswith("rccl") else None
-    comm = comms[0] if comms else None
 
     def join(j):                                             # slot j's stream waits for its gather
         if works[j] is None:
             return
-        if comm is not None:
-            k, ticket = works[j]                             # (stream/communicator index, ticket)
-            comms[k].wait(sts[k], ticket)
-        else:
-            works[j].wait()
+        k, ticket = works[j]
+        comms[k].wait(sts[k], ticket)
         works[j] = None
 
     def step(i, ns, gather=True):
         g, j, st = pops[i % N_POPS], i % RING, sts[i % ns]
         join(j)
-        plan.fitness_device(st, g.data_ptr(), POP, N_SPLATS, 9, K_SIGMA, outs[j].data_ptr())
-        if not distributed or GATHER == "none" or not gather:
+        plan.fitness_device(st, g.ptr, POP, N_SPLATS, 9, K_SIGMA, outs[j].ptr)
+        if comms is None or not gather:
             return
-        if comm is not None:                                 # RCCL: fitness scalars to every rank
-            works[j] = (i % ns, comms[i % ns].allgather(st, outs[j].data_ptr(), gathered[j].data_ptr(), POP,
-                                                        overlap=GATHER == "rccl-overlap"))
-        else:
-            works[j] = dist.all_gather_into_tensor(gathered[j], outs[j], async_op=True)
-        if GATHER == "torch-sync":
-            join(j)
+        # RCCL: fitness scalars to every rank
+        works[j] = (i % ns, comms[i % ns].allgather(st, outs[j].ptr, gathered[j].ptr, POP,
+                                                    overlap=GATHER == "rccl-overlap"))
 
     def barrier():
         for j in range(RING):
             join(j)
-        if distributed:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
+        for s in streams:
+            s.synchronize()
+        if comms is not None:
+            comms[0].barrier()
+        hip.synchronize()
 
     # Clock ramp before any measurement: the GPU raises its clocks over tens of ms
-    # of load (a 30-step run right after set-up measured the raster at 0.187-0.195
-    # ms vs 0.178 ms in steady state), so run the evaluation untimed for --ramp-ms
-    # first (no gathers: ranks may run different numbers of these steps).
+    # of load, so run the evaluation untimed for --ramp-ms first (no gathers:
+    # ranks may run different numbers of these steps).
     def ramp(ms, ns):
         t_ramp, i = time.perf_counter(), 0
         while (time.perf_counter() - t_ramp) * 1e3 < ms:
             for _ in range(50):
                 step(i, ns, gather=False)
                 i += 1
-            torch.cuda.synchronize(dev)
+            for s in streams:
+                s.synchronize()
         barrier()
 
-    barrier()                  # first collective's one-time set-up before the ramp, not after it
-    ramp(args.ramp_ms, args.streams)
+    def max_over_ranks(vals):
+        v = np.asarray(vals, np.float64)
+        if comms is None:
+            return v
+        return comms[0].allgather_host(v.astype(np.float32)).astype(np.float64).max(0)
 
     def timed(ns):
-        """W untimed + K timed steps over ns streams, bracketed by barrier + synchronize:
-        (this rank's seconds, host enqueue seconds); the max over ranks is taken
-        once every pass has run."""
+        """W untimed steps, then passes of exactly K steps, each bracketed by
+        barrier + synchronize, until --min-time seconds were measured (the same
+        number of passes on every rank).  Returns (median pass seconds after the
+        max over ranks per pass, passes, host enqueue seconds of the first pass)."""
         for i in range(args.warmup):
             step(i, ns)
         barrier()
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            step(i, ns)
-        host_s = time.perf_counter() - t0                   # enqueue time (host side)
-        barrier()
-        return time.perf_counter() - t0, host_s
 
-    elapsed, host_s = timed(args.streams)                  # the headline
-    if distributed and GATHER != "none":                    # the gather delivered this rank's shard
+        def one_pass():
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                step(i, ns)
+            host_s = time.perf_counter() - t0
+            barrier()
+            return time.perf_counter() - t0, host_s
+
+        first, host_s = one_pass()
+        reps = int(max_over_ranks([min(1000, max(1, math.ceil(args.min_time / max(first, 1e-9))))])[0])
+        passes = [first] + [one_pass()[0] for _ in range(reps - 1)]
+        per_pass = max_over_ranks(passes)
+        return float(np.median(per_pass)), len(passes), host_s
+
+    barrier()                  # first collective's one-time set-up before the ramp, not after it
+    ramp(args.ramp_ms, args.streams)
+    elapsed, passes, host_s = timed(args.streams)          # the headline
+    shard_ok = True
+    if comms is not None and GATHER != "none":             # the gather delivered this rank's shard
         j = (args.steps - 1) % RING
-        shard_ok = torch.equal(gathered[j][rank * POP:(rank + 1) * POP], outs[j])
-    # dependent batches (a GA generation needs the previous one's fitness): one stream
-    # (each later pass gets a short ramp too: under torchrun the first passes after
-    # a switch measured 5-15 % slow, tools/probe/pass_speed.py)
-    if args.streams > 1:
-        ramp(args.ramp_ms / 3, 1)
-        elapsed1, _ = timed(1)
-    else:
-        elapsed1 = elapsed
-    ramp(args.ramp_ms / 3, 1)
+        shard_ok = np.array_equal(gathered[j].to_host()[rank * POP:(rank + 1) * POP], outs[j].to_host())
 
-    # per-kernel device time (HIP events on the launch stream) over a third,
-    # single-stream pass (kernels alone, not sharing the chip with the other
-    # stream's): the raster kernel is the dominant one
-    for rep in range(int(os.environ.get("GGS_BENCH_PROFILE_REPS", "1"))):
+    extras = {}
+    kern = {}
+    if args.extras:
+        # dependent batches (a GA generation needs the previous one's fitness): one stream
+        if args.streams > 1:
+            ramp(args.ramp_ms / 3, 1)
+            elapsed1, passes1, _ = timed(1)
+        else:
+            elapsed1, passes1 = elapsed, passes
+        extras["value_one_stream"] = round(world * POP * args.steps / elapsed1, 1)
+        extras["ms_per_step_one_stream"] = round(elapsed1 / args.steps * 1e3, 4)
+        # + the D2H of the B fitness scalars each step (fitness.py:42 .cpu()) and a host sync
+        ramp(args.ramp_ms / 3, 1)
+        host_out = np.empty(POP, np.float32)
+        t0 = time.perf_counter()
+        n_rb = 0
+        while time.perf_counter() - t0 < args.min_time:
+            for i in range(args.steps):
+                step(i, 1, gather=False)
+                hip.memcpy_d2h_async(host_out, outs[i % RING].ptr, POP * 4, streams[0])
+                streams[0].synchronize()
+            n_rb += args.steps
+        rb_s = max_over_ranks([(time.perf_counter() - t0) / n_rb])[0]
+        extras["value_with_readback"] = round(world * POP / rb_s, 1)
+        barrier()
+        ramp(args.ramp_ms / 3, 1)
+
+        # per-kernel device time (HIP events on the launch stream) over a single-stream
+        # pass (kernels alone, not sharing the chip with another stream's)
         ggs.profile_reset()
         ggs.profile_enable(True)
         for i in range(args.steps):
-            step(i, 1)
+            step(i, 1, gather=False)
         barrier()
         ggs.profile_enable(False)
-        if os.environ.get("GGS_BENCH_PROFILE_REPS") and rank == 0:
-            ms_, n_ = ggs.profile_read("raster")
-            print(f"profile pass {rep}: raster {ms_ / max(n_, 1):.4f} ms", file=sys.stderr, flush=True)
-    kern = {k: ggs.profile_read(k) for k in ("prep", "raster", "finalize")}
-    raster_ms = kern["raster"][0] / max(kern["raster"][1], 1)
-    # max over ranks, after every measured pass (a first all-reduce between the
-    # passes idles the GPU long enough for the clocks to drop)
+        kern = {k: ggs.profile_read(k) for k in ("prep", "raster", "finalize")}
     if distributed:
-        t = torch.tensor([elapsed, elapsed1], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, elapsed1 = (float(v) for v in t.tolist())
-        if GATHER != "none":
-            assert shard_ok, "fitness all-gather returned a different shard"
+        assert shard_ok, "fitness all-gather returned a different shard"
 
     # algorithmic work of this workload (AABB pairs from the product's own prep)
     pairs = 0
-    for p in pops:
-        pre = ggs.preprocess(ggs.encode(p.cpu().numpy()), H, W, K_SIGMA)
+    for p in pops_h:
+        pre = ggs.preprocess(ggs.encode(p), H, W, K_SIGMA)
         pairs += int(((pre["x1"].astype(np.int64) - pre["x0"] + 1) *
                       (pre["y1"].astype(np.int64) - pre["y0"] + 1)).sum())
     pairs_per_cand = pairs / (N_POPS * POP)
@@ -358,70 +497,101 @@ def main():
     # target/mask content check, pinned staging, 3 launches, D2H) — the path a
     # caller handing over host buffers gets; reported beside, never the value
     host_api = None
-    if world == 1 and not distributed:
-        hpops = [p.cpu().numpy() for p in pops]
-        ggs.fitness(hpops[0], tgt_h, H, W, K_SIGMA, weight_mask=mask_h)
+    if world == 1 and args.extras:
+        ggs.fitness(pops_h[0], tgt_h, H, W, K_SIGMA, weight_mask=mask_h, device=local_rank)
         n_h, t_h = 0, time.perf_counter()
         while time.perf_counter() - t_h < 0.5:
-            ggs.fitness(hpops[n_h % N_POPS], tgt_h, H, W, K_SIGMA, weight_mask=mask_h)
+            ggs.fitness(pops_h[n_h % N_POPS], tgt_h, H, W, K_SIGMA, weight_mask=mask_h, device=local_rank)
             n_h += 1
         host_api = round(n_h * POP / (time.perf_counter() - t_h), 1)
 
-    total = world * POP * args.steps
+    total = global_batch * args.steps if scaling == "strong" else world * POP * args.steps
     value = total / elapsed
-    raster_bytes = bytes_per_candidate() * POP
-    achieved_gbs = raster_bytes / (raster_ms * 1e-3) / 1e9
-    valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic() if args.config == "512" and POP == 128 else (None, None)
+    ms_step = elapsed / args.steps * 1e3
+    step_bytes = bytes_per_candidate() * POP
+    roof = None
+    if kern:
+        raster_ms = kern["raster"][0] / max(kern["raster"][1], 1)
+        achieved = step_bytes / (raster_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic() if headline else (None, None)
+        valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
+        roof = {"bound": "hbm", "kernel": "raster_kernel<1, false>" if N_SPLATS <= 512 else
+                "raster_kernel<1, true>",
+                "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": None if traffic is None else round(traffic),
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": step_bytes,
+                "avg_launch_ms": round(raster_ms, 5),
+                "regime": "single-stream pass (kernels alone, HIP events on the launch stream); pairs "
+                          "with ms_per_step_one_stream, as the committed rocprofv3 trace (bench.py "
+                          "--streams 1)",
+                "rocprof_trace_avg_ms": (None if not headline or pmc_trace_avg_us() is None
+                                         else round(pmc_trace_avg_us() / 1e3, 5)),
+                "step_effective": {"regime": f"headline, {args.streams} streams (overlapping batches)",
+                                   "achieved": round(step_bytes / (ms_step * 1e-3) / 1e9, 2),
+                                   "frac": round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                                   "ms_per_step": round(ms_step, 5)},
+                "note": "VALU/transcendental-bound path (SURVEY.md §8d): see 'valu'"}
+        valu = {"achieved": round(valu_tflops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
+                "flop_per_aabb_pair": FLOP_PER_PAIR, "aabb_pairs_per_candidate": pairs_per_cand,
+                "accounting": "reference-equivalent work: 24 FLOP per AABB pair (SURVEY.md §8d); "
+                              "the row recurrence executes fewer, so frac can exceed 1",
+                "busy_pmc": pmc_valu_busy() if headline else None}
     if rank == 0:
         line = {
-            "metric": "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=128"
-                      if args.config == "512" and POP == 128 else
-                      f"candidate renders/sec, {H}x{W}, {N_SPLATS} splats, pop={POP} per GPU",
+            "metric": METRIC if headline else
+            f"candidate renders/sec, {H}x{W}, {N_SPLATS} splats, pop={global_batch}"
+            + (f" split over {world} GPU(s)" if scaling == "strong" else f" per GPU x {world}"),
             "value": round(value, 1),
             "unit": "candidate renders/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (population.py distributions, U[0,1] target, U[0.405,1] mask)",
-            "config": {"workload": f"{H}x{W} canvas, {N_SPLATS} splats/candidate, pop={POP} per GPU, "
-                                   "weighted-L2 fitness (encode+prep+raster+reduce)",
+            "config": {"workload": f"{H}x{W} canvas, {N_SPLATS} splats/candidate, "
+                                   + (f"pop={global_batch} split over {world} GPU(s) ({POP} per GPU)"
+                                      if scaling == "strong" else f"pop={POP} per GPU")
+                                   + ", weighted-L2 fitness (encode+prep+raster+reduce"
+                                   + (" + RCCL fitness all-gather)" if comms else ")"),
                        "H": H, "W": W, "splats": N_SPLATS, "pop_per_gpu": POP,
-                       "global_batch": POP * world, "parallelism": f"dp{world} (candidate shards)",
-                       "fitness_gather": (GATHER if distributed else None)},
+                       "global_batch": global_batch, "parallelism": f"dp{world} (candidate shards)",
+                       "fitness_gather": (GATHER if comms else None),
+                       "rccl_ranks": (world if comms else None)},
+            "timing": {"passes": passes, "statistic": "median pass of K steps (max over ranks per pass)",
+                       "measured_s": round(elapsed * passes, 3)},
             "gsplat_pixels_per_s": round(value * N_SPLATS * H * W / 1e9, 2),
             "aabb_pairs_per_s": round(value * pairs_per_cand, 1),
-            "roofline": {"bound": "hbm", "kernel": "raster_kernel<1, false>",
-                         "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
-                         "traffic": None if traffic is None else round(traffic),
-                         "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": raster_bytes,
-                         "avg_launch_ms": round(raster_ms, 5),
-                         "note": "VALU/transcendental-bound path (SURVEY.md §8d): see 'valu'"},
-            "valu": {"achieved": round(valu_tflops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
-                     "flop_per_aabb_pair": FLOP_PER_PAIR, "aabb_pairs_per_candidate": pairs_per_cand,
-                     "accounting": "reference-equivalent work: 24 FLOP per AABB pair (SURVEY.md §8d); "
-                                   "the row recurrence executes fewer, so frac can exceed 1",
-                     "busy_pmc": pmc_valu_busy() if args.config == "512" and POP == 128 else None},
+            "roofline": roof,
+            "valu": valu if kern else None,
             "streams": args.streams,
-            "value_one_stream": round(world * POP * args.steps / elapsed1, 1),
+            **extras,
             "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "host_api_renders_per_s": host_api,
             "kernels_ms_per_launch": {k: round(v[0] / max(v[1], 1), 5) for k, v in kern.items()},
+            "hip_runtime": _mapped("libamdhip64"),
+            "torch_loaded": "torch" in sys.modules,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     for c in comms or ():
         c.close()
-    if distributed:
-        dist.destroy_process_group()
+
+
+def _mapped(name):
+    try:
+        for line in open("/proc/self/maps"):
+            if name in line:
+                return line.split()[-1]
+    except OSError:
+        pass
+    return None
 
 
 if __name__ == "__main__":

@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -292,6 +293,10 @@ int check_dims(int64_t B, int32_t N, int32_t C, int32_t H, int32_t W) {
     if (B < 0 || N < 0) return fail(GGS_EINVAL, "B=%lld and N=%d must be >= 0", (long long)B, N);
     if (C < 9) return fail(GGS_EINVAL, "expected at least 9 genome cols, got C=%d (render.py:223)", C);
     if (H < 1 || W < 1) return fail(GGS_EINVAL, "H=%d, W=%d must be >= 1", H, W);
+    // the raster's cull list holds 32-bit byte offsets of 64-B records: N * 64 < 2^31
+    if ((int64_t)N * (int64_t)sizeof(SplatRec) >= ((int64_t)1 << 31))
+        return fail(GGS_EINVAL, "N=%d splats per candidate exceeds the limit %lld", N,
+                    (long long)(((int64_t)1 << 31) / (int64_t)sizeof(SplatRec) - 1));
     int nTX;
     const int64_t nTiles = raster_tiles(H, W, &nTX);
     if (B * nTiles * 4 >= (int64_t)1 << 31)
@@ -382,12 +387,37 @@ int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, 
     return GGS_OK;
 }
 
-// Split [0, B) into n contiguous shards.
+// Split [0, B) into n contiguous shards of ceil(B/n) (the last ones shorter or
+// empty): equal-sized slots, so the fitness shards meet in one in-place RCCL
+// all-gather (ggs/parallel.py shard_bounds: the same rule).
 void shard(int64_t B, int n, int d, int64_t* b0, int64_t* nb) {
-    const int64_t base = B / n, rem = B % n;
-    *b0 = d * base + std::min<int64_t>(d, rem);
-    *nb = base + (d < rem ? 1 : 0);
+    const int64_t per = (B + n - 1) / n;
+    *b0 = std::min<int64_t>(B, d * per);
+    *nb = std::min<int64_t>(B, *b0 + per) - *b0;
 }
+
+// Single-process communicators over the active device list (host-API fan-out),
+// made on first use with ggs_comm_init_local and remade when the list changes.
+std::vector<int> g_comm_devs;
+std::vector<void*> g_comms;
+
+int local_comms_locked(const std::vector<DevCtx*>& cs, std::vector<void*>* out) {
+    std::vector<int> devs;
+    for (DevCtx* c : cs) devs.push_back(c->dev);
+    if (devs != g_comm_devs) {
+        for (void* c : g_comms) ggs_comm_destroy(c);
+        g_comms.clear();
+        g_comm_devs.clear();
+        std::vector<void*> made(devs.size(), nullptr);
+        const int rc = ggs_comm_init_local((int32_t)devs.size(), devs.data(), made.data());
+        if (rc) return rc;
+        g_comms = made;
+        g_comm_devs = devs;
+    }
+    *out = g_comms;
+    return GGS_OK;
+}
+std::mutex g_comm_mu;
 
 }  // namespace
 }  // namespace ggs
@@ -430,6 +460,12 @@ int ggs_select_devices(const int32_t* ids, int32_t n) {
 const char* ggs_last_error(void) { return t_err.c_str(); }
 
 void ggs_shutdown(void) {
+    {
+        std::lock_guard<std::mutex> cl(g_comm_mu);
+        for (void* c : g_comms) ggs_comm_destroy(c);
+        g_comms.clear();
+        g_comm_devs.clear();
+    }
     std::lock_guard<std::mutex> lk(g_mu);
     {
         std::lock_guard<std::mutex> pl(g_prof_mu);
@@ -577,17 +613,25 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
     const uint64_t tkey = hash_bytes(target_hw3, tbytes);
     const uint64_t mkey = mask_hw ? hash_bytes(mask_hw, mbytes) : 0;
     const size_t row = (size_t)N * C;
+    const int64_t per = (B + nd - 1) / nd;
+    // RCCL gather of the shards (GGS_FANOUT_RCCL=1 forces it at one device: tests)
+    static const bool force_rccl = getenv("GGS_FANOUT_RCCL") && atoi(getenv("GGS_FANOUT_RCCL")) != 0;
+    const bool gather = nd > 1 || force_rccl;
 
     std::vector<std::unique_lock<std::mutex>> locks;
     for (int d = 0; d < nd; ++d) locks.emplace_back(cs[d]->mu);
-    // enqueue on every device, then wait on every device
+    // enqueue on every device, then gather (nd > 1) and wait
     for (int d = 0; d < nd; ++d) {
         DevCtx* c = cs[d];
         int64_t b0, nb;
         shard(B, nd, d, &b0, &nb);
-        if (nb == 0) continue;
         DeviceGuard dg(c->dev);
         hipStream_t st = c->stream;
+        // one slot per device for the in-place gather (nd == 1: just this shard);
+        // devices without candidates still take part in the gather
+        if ((rc = ensure(c->out, sizeof(float) * (size_t)per * nd, st))) return rc;
+        if ((rc = ensure_pinned(c->h_out, sizeof(float) * (size_t)(gather ? B : nb)))) return rc;
+        if (nb == 0) continue;
         if ((rc = ensure(c->target, tbytes, st))) return rc;
         if (tkey != c->target_key || tbytes != c->target_bytes) {
             GGS_HIP(hipMemcpyAsync(c->target.p, target_hw3, tbytes, hipMemcpyHostToDevice, st));
@@ -604,9 +648,7 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
         }
         const size_t gbytes = sizeof(float) * row * (size_t)nb;
         if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
-        if ((rc = ensure(c->out, sizeof(float) * nb, st))) return rc;
         if ((rc = ensure_pinned(c->h_gen, std::max<size_t>(gbytes, 4)))) return rc;
-        if ((rc = ensure_pinned(c->h_out, sizeof(float) * nb))) return rc;
         GGS_HIP(hipStreamSynchronize(st));  // pinned staging may still feed a previous copy
         if (gbytes) {
             memcpy(c->h_gen.p, genomes_axes + row * b0, gbytes);
@@ -619,19 +661,37 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
                                ((uint64_t)W << 20)) & ~(1ull << 63);
         if ((rc = run_fitness(c, st, (const float*)c->gen.p, nb, N, C, (const float*)c->target.p,
                               mask_hw ? (const float*)c->mask.p : nullptr, mode, boost_beta, H, W,
-                              k_sigma, (float*)c->out.p, pkey | 1)))
+                              k_sigma, (float*)c->out.p + (gather ? b0 : 0), pkey | 1)))
             return rc;
-        GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, sizeof(float) * nb, hipMemcpyDeviceToHost, st));
+        if (!gather)
+            GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, sizeof(float) * nb, hipMemcpyDeviceToHost, st));
     }
-    for (int d = 0; d < nd; ++d) {
-        DevCtx* c = cs[d];
-        int64_t b0, nb;
-        shard(B, nd, d, &b0, &nb);
-        if (nb == 0) continue;
-        DeviceGuard dg(c->dev);
-        GGS_HIP(hipStreamSynchronize(c->stream));
-        memcpy(out_B + b0, c->h_out.p, sizeof(float) * nb);
+    if (gather) {
+        // north_star: one RCCL gather of the shards' fitness scalars (in place, every
+        // device's out[] becomes the whole vector), then ONE D2H from the first device
+        std::lock_guard<std::mutex> cl(g_comm_mu);
+        std::vector<void*> comms;
+        if ((rc = local_comms_locked(cs, &comms))) return rc;
+        std::vector<hipStream_t> sts;
+        std::vector<float*> bufs;
+        for (DevCtx* c : cs) {
+            sts.push_back(c->stream);
+            bufs.push_back((float*)c->out.p);
+        }
+        if ((rc = comm_group_allgather_inplace(comms.data(), nd, sts.data(), bufs.data(), per))) return rc;
+        DeviceGuard dg(cs[0]->dev);
+        GGS_HIP(hipMemcpyAsync(cs[0]->h_out.p, cs[0]->out.p, sizeof(float) * B, hipMemcpyDeviceToHost,
+                               cs[0]->stream));
+        for (int d = nd - 1; d >= 0; --d) {     // every device's gather done (the first: and its D2H)
+            DeviceGuard dg2(cs[d]->dev);
+            GGS_HIP(hipStreamSynchronize(cs[d]->stream));
+        }
+        memcpy(out_B, cs[0]->h_out.p, sizeof(float) * B);
+        return GGS_OK;
     }
+    DeviceGuard dg(cs[0]->dev);
+    GGS_HIP(hipStreamSynchronize(cs[0]->stream));
+    memcpy(out_B, cs[0]->h_out.p, sizeof(float) * B);
     return GGS_OK;
 }
 
@@ -809,6 +869,7 @@ struct GaSession {
     int64_t n_curves = 0, curves_cap = 0;
     void* comm = nullptr;          // ggs_ga_set_comm: offspring fitness sharded over ranks
     int nranks = 1, rank = 0;
+    uint64_t fingerprint = 0;      // hash of (config, target, mask, initial population)
 };
 
 double anneal_factor(int gen, int total, int kind) {          // utils.py:14-27
@@ -1059,6 +1120,11 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     s->P = c.pop_size;
     s->N = c.n_splats;
     const size_t pb = sizeof(float) * 9 * (size_t)s->P * s->N, hw = (size_t)c.H * c.W;
+    // what every rank of a sharded session must agree on (ggs_ga_set_comm checks it)
+    s->fingerprint = hash_bytes(&s->cfg, sizeof s->cfg) * 0x9E3779B97F4A7C15ull ^
+                     hash_bytes(target_hw3, sizeof(float) * 3 * hw) * 0xC2B2AE3D27D4EB4Full ^
+                     (mask_hw ? hash_bytes(mask_hw, sizeof(float) * hw) : 0x165667B19E3779F9ull) ^
+                     rotl(hash_bytes(init_pop, pb), 29);
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard dg(ctx->dev);
     auto bail = [&](int code) { ga_free(s.get()); return code; };
@@ -1118,6 +1184,20 @@ int ggs_ga_set_comm(void* handle, void* comm) {
     if (comm) {
         int rc = ggs_comm_size(comm, &n, &r);
         if (rc) return rc;
+        // the ranks must breed identical offspring: compare the sessions' fingerprints
+        // (exchanged as two float32 bit patterns; an all-gather only moves bytes)
+        float mine[2];
+        memcpy(mine, &s->fingerprint, sizeof mine);
+        std::vector<float> all(2 * (size_t)n);
+        if ((rc = ggs_comm_allgather_host(comm, mine, all.data(), 2))) return rc;
+        for (int k = 0; k < n; ++k) {
+            uint64_t f;
+            memcpy(&f, &all[2 * (size_t)k], sizeof f);
+            if (f != s->fingerprint)
+                return fail(GGS_EINVAL, "ggs_ga_set_comm: rank %d's session differs from rank %d's (config, "
+                            "target, mask, initial population or seed): the shards would mix populations",
+                            k, r);
+        }
     }
     std::lock_guard<std::mutex> lk(s->c->mu);
     DeviceGuard dg(s->c->dev);

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/ggs.h"
 
@@ -42,6 +43,9 @@ struct Rccl {
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
     std::string err;
     bool ok = false;
@@ -64,9 +68,14 @@ const Rccl& rccl() {
         r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
         r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
         r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-        r.ok = r.get_unique_id && r.comm_init_rank && r.all_gather && r.comm_destroy && r.error_string;
+        r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
+        r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+        r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+        r.ok = r.get_unique_id && r.comm_init_rank && r.all_gather && r.comm_destroy && r.error_string &&
+               r.comm_init_all && r.group_start && r.group_end;
         if (!r.ok) r.err = "RCCL is missing an entry point (ncclGetUniqueId / ncclCommInitRank / "
-                           "ncclAllGather / ncclCommDestroy / ncclGetErrorString)";
+                           "ncclCommInitAll / ncclAllGather / ncclGroupStart / ncclGroupEnd / "
+                           "ncclCommDestroy / ncclGetErrorString)";
     });
     return r;
 }
@@ -92,8 +101,32 @@ struct Comm {
     hipEvent_t ready = nullptr;          // caller's stream -> side
     hipEvent_t done[kTickets] = {};      // side -> caller's stream, one per ticket slot
     int64_t issued = 0;                  // tickets handed out
+    float* scratch = nullptr;            // barrier / host all-gather staging (device)
+    int64_t scratch_cap = 0;             // floats
     std::mutex mu;
 };
+
+// Staging for the host-pointer collectives: [count | nranks*count] floats.
+int ensure_scratch(Comm* c, int64_t floats) {
+    if (floats <= c->scratch_cap) return GGS_OK;
+    if (c->scratch) (void)hipFree(c->scratch);
+    c->scratch = nullptr;
+    c->scratch_cap = 0;
+    const int64_t want = std::max<int64_t>(floats, 1024);
+    GGS_HIPC(hipMalloc((void**)&c->scratch, sizeof(float) * (size_t)want));
+    c->scratch_cap = want;
+    return GGS_OK;
+}
+
+// Finish a freshly made communicator (its side stream and events).
+int comm_setup(Comm* c) {
+    hipError_t he = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
+    for (int i = 0; he == hipSuccess && i < kTickets; ++i)
+        he = hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming);
+    if (he != hipSuccess) return cfail(GGS_EHIP, "communicator set-up: %s", hipGetErrorString(he));
+    return GGS_OK;
+}
 
 // A gather over one rank is a copy: done by a small kernel on the stream, not
 // through RCCL (whose single-rank path costs a stream-ordering round trip).
@@ -145,12 +178,7 @@ int ggs_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t*
     int rc = GGS_OK;
     ncclResult_t nr = R.comm_init_rank(&c->nc, nranks, u, rank);
     if (nr != ncclSuccess) rc = cfail(GGS_EHIP, "ncclCommInitRank: %s", R.error_string(nr));
-    hipError_t he = hipSuccess;
-    if (!rc) he = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-    if (!rc && he == hipSuccess) he = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
-    for (int i = 0; !rc && he == hipSuccess && i < kTickets; ++i)
-        he = hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming);
-    if (!rc && he != hipSuccess) rc = cfail(GGS_EHIP, "ggs_comm_create: %s", hipGetErrorString(he));
+    if (!rc) rc = comm_setup(c);
     if (rc) {
         ggs_comm_destroy(c);
         return rc;
@@ -226,8 +254,98 @@ void ggs_comm_destroy(void* comm) {
             if (c->done[i]) (void)hipEventDestroy(c->done[i]);
         if (c->ready) (void)hipEventDestroy(c->ready);
         if (c->side) (void)hipStreamDestroy(c->side);
+        if (c->scratch) (void)hipFree(c->scratch);
     }
     delete c;
 }
 
+int ggs_comm_init_local(int32_t n, const int32_t* devices, void** comms) {
+    const Rccl& R = rccl();
+    if (!R.ok) return cfail(GGS_ENODEV, "%s", R.err.c_str());
+    if (n < 1 || !devices || !comms) return cfail(GGS_EINVAL, "ggs_comm_init_local: need n >= 1 devices and outputs");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    for (int i = 0; i < n; ++i) {
+        if (devices[i] < 0 || devices[i] >= ndev)
+            return cfail(GGS_ENODEV, "ggs_comm_init_local: device %d not available (%d visible)", devices[i], ndev);
+        for (int j = 0; j < i; ++j)
+            if (devices[j] == devices[i]) return cfail(GGS_EINVAL, "ggs_comm_init_local: device %d listed twice", devices[i]);
+    }
+    std::vector<ncclComm_t> ncs(n, nullptr);
+    {
+        ncclResult_t nr = R.comm_init_all(ncs.data(), n, devices);
+        if (nr != ncclSuccess) return cfail(GGS_EHIP, "ncclCommInitAll: %s", R.error_string(nr));
+    }
+    int rc = GGS_OK;
+    for (int i = 0; i < n; ++i) {
+        Comm* c = new Comm;
+        c->dev = devices[i];
+        c->nranks = n;
+        c->rank = i;
+        c->nc = ncs[i];
+        comms[i] = c;
+        if (!rc) {
+            DevScope ds(c->dev);
+            rc = comm_setup(c);
+        }
+    }
+    if (rc) {
+        for (int i = 0; i < n; ++i) { ggs_comm_destroy(comms[i]); comms[i] = nullptr; }
+        return rc;
+    }
+    return GGS_OK;
+}
+
+int ggs_comm_allgather_host(void* comm, const float* send, float* recv, int64_t count) {
+    const Rccl& R = rccl();
+    Comm* c = (Comm*)comm;
+    if (!c || !R.ok) return cfail(GGS_EINVAL, "ggs_comm_allgather_host: no communicator");
+    if (count < 0 || (count > 0 && (!send || !recv)))
+        return cfail(GGS_EINVAL, "ggs_comm_allgather_host: count %lld with null buffers", (long long)count);
+    std::lock_guard<std::mutex> lk(c->mu);
+    DevScope ds(c->dev);
+    const int64_t cnt = std::max<int64_t>(count, 1);    // a zero-length call still synchronises the ranks
+    int rc = ensure_scratch(c, cnt * (1 + c->nranks));
+    if (rc) return rc;
+    float* d_send = c->scratch;
+    float* d_recv = c->scratch + cnt;
+    if (count > 0)
+        GGS_HIPC(hipMemcpyAsync(d_send, send, sizeof(float) * (size_t)count, hipMemcpyHostToDevice, c->side));
+    else
+        GGS_HIPC(hipMemsetAsync(d_send, 0, sizeof(float), c->side));
+    GGS_NCCL(R.all_gather(d_send, d_recv, (size_t)cnt, ncclFloat32, c->nc, c->side));
+    if (count > 0) {
+        for (int r = 0; r < c->nranks; ++r)
+            GGS_HIPC(hipMemcpyAsync(recv + (int64_t)r * count, d_recv + (int64_t)r * cnt, sizeof(float) * (size_t)count,
+                                    hipMemcpyDeviceToHost, c->side));
+    }
+    GGS_HIPC(hipStreamSynchronize(c->side));
+    return GGS_OK;
+}
+
+int ggs_comm_barrier(void* comm) { return ggs_comm_allgather_host(comm, nullptr, nullptr, 0); }
+
 }  // extern "C"
+
+namespace ggs {
+// Single-process fan-out (ggs_capi.cpp): one in-place all-gather per device of
+// that device's `per`-float shard of buf[d] (shard d at buf[d] + d*per), grouped
+// so one thread can drive every device.
+int comm_group_allgather_inplace(void* const* comms, int n, hipStream_t const* streams, float* const* bufs,
+                                 int64_t per) {
+    const Rccl& R = rccl();
+    if (!R.ok) return cfail(GGS_ENODEV, "%s", R.err.c_str());
+    GGS_NCCL(R.group_start());
+    ncclResult_t first_err = ncclSuccess;
+    for (int d = 0; d < n; ++d) {
+        Comm* c = (Comm*)comms[d];
+        DevScope ds(c->dev);
+        ncclResult_t r = R.all_gather(bufs[d] + (int64_t)c->rank * per, bufs[d], (size_t)per, ncclFloat32, c->nc,
+                                      streams[d]);
+        if (r != ncclSuccess && first_err == ncclSuccess) first_err = r;
+    }
+    GGS_NCCL(R.group_end());
+    if (first_err != ncclSuccess) return cfail(GGS_EHIP, "ncclAllGather: %s", R.error_string(first_err));
+    return GGS_OK;
+}
+}  // namespace ggs

@@ -96,4 +96,10 @@ hipError_t launch_ga_gather(hipStream_t st, const float* pop, const float* off, 
                             const int* src, float* next, const GaBestDev& best, int init);
 int ga_max_population();
 
+// ---- RCCL (ggs_comm.cpp) ----------------------------------------------------
+// Grouped in-place all-gather over single-process communicators (ggs_comm_init_local):
+// buf[d] holds shard d at buf[d] + d*per; afterwards every buf[d] holds all n shards.
+int comm_group_allgather_inplace(void* const* comms, int n, hipStream_t const* streams, float* const* bufs,
+                                 int64_t per);
+
 }  // namespace ggs

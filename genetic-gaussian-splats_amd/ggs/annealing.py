@@ -75,6 +75,8 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
     most strips are dirty anyway and the bookkeeping costs more than it saves,
     DESIGN.md §9)."""
     from .mask import compute_importance_mask, prepare_target
+    from .ga import resolve_seed
+    seed = resolve_seed(seed)                                # run_sags.py:26-27 seeds `random`
     sched = temp_schedule
     t = prepare_target(target_img_uint8, H, W)                       # annealing.py:87
     imp_mask = compute_importance_mask(t, H, W, edge_scales=(1, 2, 4), w_edge=0.7, w_var=0.3,
@@ -86,7 +88,8 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
         from . import api
 
         def evaluate(G):
-            return api.fitness(G, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only)
+            return api.fitness(G, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only,
+                               device=device)
     explicit = draws is not None
     draws = draws if draws is not None else NumpyDraws(seed)
     curr = (np.array(init_individual, np.float32, copy=True) if init_individual is not None else
@@ -97,7 +100,7 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
     if backend == "device":
         prop = _DeviceProposer(t, imp_mask, curr, max(1, tries), mutpb, mut_sigma_max,
                                mut_sigma_min, sigma_schedule, min_scale_splats, max_scale_splats,
-                               k_sigma, boost_only, seed, incremental)
+                               k_sigma, boost_only, seed, incremental, device)
     elif backend == "host":
         prop = _HostProposer(curr, evaluate, iterations, sigma_schedule, mut_sigma_max,
                              mut_sigma_min, mutpb, H, W, min_scale_splats, max_scale_splats)
@@ -234,13 +237,14 @@ class _DeviceProposer:
     """Neighbours mutated and evaluated on the GPU (ggs_sa_*)."""
 
     def __init__(self, t, mask, curr, max_tries, mutpb, sig_max, sig_min, schedule, min_s, max_s,
-                 k_sigma, boost_only, seed, incremental=False):
+                 k_sigma, boost_only, seed, incremental=False, device=None):
+        from . import api
         from .ga_device import DeviceSA
         self.sa = DeviceSA(t, mask, curr, max_tries=max_tries, mutpb=mutpb, mut_sigma_max=sig_max,
                            mut_sigma_min=sig_min, schedule=schedule, min_scale_splats=min_s,
                            max_scale_splats=max_s, k_sigma=k_sigma, boost_only=boost_only,
-                           seed=(int(np.random.SeedSequence().entropy) if seed is None
-                                 else int(seed)) & (2**64 - 1), incremental=incremental)
+                           seed=int(seed) & (2**64 - 1), incremental=incremental,
+                           device=api.device_index(device))
         self.init_fit = float(self.sa.init_fit)
 
     def stats(self):

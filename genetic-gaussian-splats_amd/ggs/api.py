@@ -8,6 +8,8 @@ unchanged.  Every compute call goes through ctypes into libggs.so.
 from __future__ import annotations
 
 import ctypes as C
+import os
+import threading
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -41,24 +43,79 @@ def _genomes3d(genomes, what: str) -> np.ndarray:
     return g
 
 
+def device_index(device=None) -> int:
+    """The HIP device a reference-style ``device`` argument names (render.py:215-217
+    resolves ``device or 'cuda'`` the same way): an explicit index ('cuda:k',
+    torch.device('cuda', k), k) wins; without one, LOCAL_RANK under a launcher
+    (one process per GPU), else device 0.  Never "every GPU"."""
+    idx = None
+    if isinstance(device, int):
+        idx = device
+    elif isinstance(device, str):
+        parts = device.split(":")
+        if len(parts) == 2 and parts[1].strip().isdigit():
+            idx = int(parts[1])
+    elif device is not None:                                   # torch.device (duck-typed)
+        idx = getattr(device, "index", None)
+    if idx is None:
+        idx = int(os.environ.get("LOCAL_RANK", "0") or 0)
+    return int(idx)
+
+
+_selected = [None]                  # the device list last handed to ggs_select_devices
+_sel_lock = threading.Lock()
+
+
+def _use_devices(device, n_devices: int) -> int:
+    """Point the host API at the devices of one call and return the n_devices
+    argument for the C layer.  n_devices == 1 (default): the single device
+    ``device`` names; n_devices > 1: fan the batch out over the first n_devices
+    GPUs (opt-in; one RCCL gather returns the scalars); n_devices <= 0: all GPUs."""
+    n = _lib.ensure_init()
+    if n_devices == 1:
+        ids = (device_index(device),)
+        if not 0 <= ids[0] < n:
+            raise _lib.GGSDeviceError(f"device {device!r} -> HIP device {ids[0]}, but {n} visible")
+    else:
+        ids = tuple(range(n if n_devices <= 0 else min(int(n_devices), n)))
+    with _sel_lock:
+        if _selected[0] != ids:
+            _lib.select_devices(list(ids))
+            _selected[0] = ids
+    return len(ids)
+
+
 def render(genomes, H: int, W: int, *, k_sigma: float = 3.0,
-           background=(1.0, 1.0, 1.0), n_devices: int = 0) -> np.ndarray:
-    """render.py:203-252 → float32 [B,H,W,3] in [0,1] (renderer-layout genomes)."""
+           background=(1.0, 1.0, 1.0), device=None, n_devices: int = 1,
+           fp16_canvas: bool = False) -> np.ndarray:
+    """render.py:203-252 → float32 [B,H,W,3] in [0,1] (renderer-layout genomes).
+
+    ``fp16_canvas`` (render.py:213 ``use_fp16_canvas``): the reference's canvas is
+    then float16 — the background is stored in half precision, the Triton kernel
+    blends in fp32 registers and stores each pixel once as float16 (round to
+    nearest even), then clamps and converts back (render.py:234-237, :252).
+    Here: background rounded to half, fp32 render, result rounded to half."""
     g = _genomes3d(genomes, "render")
     B, N, Cc = g.shape
     H, W = int(H), int(W)
-    _lib.ensure_init()
+    nd = _use_devices(device, n_devices)
     out = np.empty((B, H, W, 3), np.float32)
     bg = np.ascontiguousarray(np.broadcast_to(np.asarray(background, np.float32), (3,)))
-    check(lib.ggs_render(_fp(g), B, N, Cc, H, W, float(k_sigma), _fp(bg), _fp(out),
-                         int(n_devices)), "ggs_render")
+    if fp16_canvas:
+        bg = bg.astype(np.float16).astype(np.float32)
+    check(lib.ggs_render(_fp(g), B, N, Cc, H, W, float(k_sigma), _fp(bg), _fp(out), nd),
+          "ggs_render")
+    if fp16_canvas:
+        out = out.astype(np.float16).astype(np.float32)
     return out
 
 
 def fitness(genomes_axes, target, H: int, W: int, k_sigma: float = 3.0,
             weight_mask=None, boost_only: bool = False, boost_beta: float = 1.0,
-            n_devices: int = 0) -> np.ndarray:
-    """fitness.py:7-31 on a stacked [B,N,C] axes-angle batch → float32 [B]."""
+            device=None, n_devices: int = 1) -> np.ndarray:
+    """fitness.py:7-31 on a stacked [B,N,C] axes-angle batch → float32 [B]
+    (on the GPU ``device`` names; ``n_devices`` > 1 opts into the multi-GPU
+    fan-out, see ``_use_devices``)."""
     g = _genomes3d(genomes_axes, "fitness")
     B, N, Cc = g.shape
     H, W = int(H), int(W)
@@ -73,10 +130,10 @@ def fitness(genomes_axes, target, H: int, W: int, k_sigma: float = 3.0,
             raise GGSInputError(f"weight_mask must be [H,W] = {(H, W)}, got {tuple(mask.shape)}")
         mode = _lib.GGS_FIT_BOOST if boost_only else _lib.GGS_FIT_WEIGHTED
         mask_p = _fp(mask)
-    _lib.ensure_init()
+    nd = _use_devices(device, n_devices)
     out = np.empty((B,), np.float32)
     check(lib.ggs_fitness(_fp(g), B, N, Cc, _fp(tgt), mask_p, mode, float(boost_beta), H, W,
-                          float(k_sigma), _fp(out), int(n_devices)), "ggs_fitness")
+                          float(k_sigma), _fp(out), nd), "ggs_fitness")
     return out
 
 
@@ -90,7 +147,7 @@ def encode(G_axes) -> np.ndarray:
     lead = g.shape[:-1]
     flat = np.ascontiguousarray(g.reshape(-1, g.shape[-1]))
     out = np.empty((flat.shape[0], 9), np.float32)
-    _lib.ensure_init()
+    _use_devices(None, 1)
     check(lib.ggs_encode(_fp(flat), flat.shape[0], flat.shape[1], _fp(out)), "ggs_encode")
     return out.reshape(*lead, 9)
 
@@ -104,7 +161,7 @@ def preprocess(genome, H: int, W: int, k_sigma: float = 3.0) -> Dict[str, np.nda
     S = g.shape[0]
     f9 = np.empty((9, S), np.float32)
     i4 = np.empty((4, S), np.int32)
-    _lib.ensure_init()
+    _use_devices(None, 1)
     check(lib.ggs_preprocess(_fp(g), S, g.shape[1], int(H), int(W), float(k_sigma), _fp(f9),
                              i4.ctypes.data_as(_i32p)), "ggs_preprocess")
     keys = ("cx", "cy", "sxx", "sxy", "syy", "rc", "gc", "bc", "a")
@@ -115,18 +172,18 @@ def preprocess(genome, H: int, W: int, k_sigma: float = 3.0) -> Dict[str, np.nda
 
 def fitness_population(population: Sequence, target, H: int, W: int, k_sigma: float = 3.0,
                        chunk: Optional[int] = None, weight_mask=None,
-                       boost_only: bool = False, n_devices: int = 0) -> List[float]:
+                       boost_only: bool = False, device=None, n_devices: int = 1) -> List[float]:
     """fitness.py:34-47 → List[float]; chunking only bounds the batch size."""
     if len(population) == 0:
         return []
     G = np.stack([as_f32(p) for p in population], 0)
     if chunk is None or chunk >= len(population):
         return fitness(G, target, H, W, k_sigma, weight_mask, boost_only,
-                       n_devices=n_devices).tolist()
+                       device=device, n_devices=n_devices).tolist()
     out: List[float] = []
     for i in range(0, len(population), int(chunk)):
         out.extend(fitness(G[i:i + chunk], target, H, W, k_sigma, weight_mask, boost_only,
-                           n_devices=n_devices).tolist())
+                           device=device, n_devices=n_devices).tolist())
     return out
 
 

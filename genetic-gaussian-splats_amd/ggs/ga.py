@@ -28,6 +28,7 @@ from __future__ import annotations
 import csv
 import math
 import os
+import random
 import statistics
 from typing import Callable, Dict, Optional, Sequence, Tuple
 
@@ -92,11 +93,28 @@ def clamp_genome(G: np.ndarray, H: int, W: int, min_scale_splats: float,
 # ---------------------------------------------------------------------------
 # draw sources
 # ---------------------------------------------------------------------------
+def resolve_seed(seed: Optional[int] = None) -> int:
+    """An explicit seed, or — when None — one drawn from Python's global ``random``
+    state, so that ``random.seed(SEED)`` in the reference's entry scripts
+    (run_ggs.py:25-28, run_sags.py:26-27) makes a run repeatable here too."""
+    return int(seed) if seed is not None else random.getrandbits(63)
+
+
 class NumpyDraws:
-    """Batched draws with the distributions of the reference's RNG calls."""
+    """Batched draws with the distributions of the reference's RNG calls.  With
+    ``seed=None`` the generator is seeded from Python's ``random`` at first use
+    (``resolve_seed``), not at construction: module-level sources made at import
+    time still follow a later ``random.seed``."""
 
     def __init__(self, seed: Optional[int] = None):
-        self.rng = np.random.default_rng(seed)
+        self._seed = seed
+        self._rng = None
+
+    @property
+    def rng(self) -> np.random.Generator:
+        if self._rng is None:
+            self._rng = np.random.default_rng(resolve_seed(self._seed))
+        return self._rng
 
     def tournament(self, P: int, k: int) -> np.ndarray:           # random.randrange (genetic.py:11)
         return self.rng.integers(0, P, (P, k))
@@ -138,7 +156,7 @@ class NumpyDraws:
 def new_population(batch_size: int, n_splats: int, H: int, W: int, min_scale_splats: float,
                    max_scale_splats: float, rng: Optional[np.random.Generator] = None) -> np.ndarray:
     """[B, N, 9] axes-angle genomes with population.py's distributions."""
-    rng = rng if rng is not None else np.random.default_rng()
+    rng = rng if rng is not None else np.random.default_rng(resolve_seed())
     B, N = batch_size, n_splats
     s_lo, s_hi = float(min_scale_splats), float(max_scale_splats * float(max(H, W)))
 
@@ -255,10 +273,10 @@ def next_generation(pop: np.ndarray, fits: np.ndarray, draws, gen: int, generati
                         mutpb, H, W, min_scale_splats, max_scale_splats)
 
 
-def _render_best_u8(best: np.ndarray, H: int, W: int, k_sigma: float) -> np.ndarray:
+def _render_best_u8(best: np.ndarray, H: int, W: int, k_sigma: float, device=None) -> np.ndarray:
     """utils.py:48-58: render one axes-angle genome to uint8 [H, W, 3]."""
     from . import api
-    img = api.render(api.encode(best[None]), H, W, k_sigma=k_sigma)[0]
+    img = api.render(api.encode(best[None]), H, W, k_sigma=k_sigma, device=device)[0]
     return (np.clip(img, 0, 1) * 255.0).astype(np.uint8)
 
 
@@ -269,7 +287,7 @@ def save_frame_png(gen: int, ind, pad: int, prefix: str, video_dir: str, H: int,
         return
     from PIL import Image
     fname = f"{prefix}_{gen:0{pad}d}.png"
-    Image.fromarray(_render_best_u8(np.asarray(ind, np.float32), H, W, k_sigma)).save(
+    Image.fromarray(_render_best_u8(np.asarray(ind, np.float32), H, W, k_sigma, device)).save(
         os.path.join(video_dir, fname))
 
 
@@ -346,6 +364,7 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
     given)."""
     from .mask import compute_importance_mask, prepare_target
 
+    seed = resolve_seed(seed)                                          # run_ggs.py:25-28 seeds `random`
     t = prepare_target(target_img_uint8, H, W)                         # algorithm.py:33-39
     imp_mask = compute_importance_mask(t, H, W, edge_scales=(1, 2, 4), w_edge=0.7, w_var=0.3,
                                        gamma=0.7, floor=0.15, smooth=3,
@@ -354,7 +373,8 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
         from . import api
 
         def evaluate(G):
-            return api.fitness(G, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only)
+            return api.fitness(G, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only,
+                               device=device)
     pop = (np.array(init_population, np.float32, copy=True) if init_population is not None else
            new_population(pop_size, n_splats, H, W, min_scale_splats, max_scale_splats,
                           np.random.default_rng(seed)))
@@ -366,7 +386,7 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
                                       min_scale_splats, max_scale_splats, k_sigma, boost_only,
                                       save_video, frame_every, video_dir, prefix, loss_png_path,
                                       loss_csv_path, loss_log_y, seed, draws, progress,
-                                      return_state, chunk)
+                                      return_state, chunk, device)
     if backend != "host":
         raise ValueError(f"backend must be 'host' or 'device', got {backend!r}")
     draws = draws if draws is not None else NumpyDraws(seed)
@@ -434,8 +454,10 @@ def _genetic_approx_device(t, imp_mask, pop, H, W, generations, tour_k, elite_k,
                            mut_sigma_max, mut_sigma_min, schedule, min_scale_splats,
                            max_scale_splats, k_sigma, boost_only, save_video, frame_every,
                            video_dir, prefix, loss_png_path, loss_csv_path, loss_log_y, seed,
-                           draws, progress, return_state, chunk):
-    """genetic_approx with backend="device" (ggs/ga_device.py)."""
+                           draws, progress, return_state, chunk, device=None):
+    """genetic_approx with backend="device" (ggs/ga_device.py) on the GPU
+    ``device`` names (api.device_index)."""
+    from . import api
     from .ga_device import run_device_ga
     pad = len(str(generations))
     every = max(1, frame_every)
@@ -457,14 +479,14 @@ def _genetic_approx_device(t, imp_mask, pop, H, W, generations, tour_k, elite_k,
         state["gen"] = gen
         if save_video and gen % every == 0:
             st = ga.read()
-            save_frame_png(gen, st["best"], pad, prefix, video_dir, H, W, k_sigma, None, save_video)
+            save_frame_png(gen, st["best"], pad, prefix, video_dir, H, W, k_sigma, device, save_video)
         if bar is not None:
             bar.set_postfix(sigma_fac=f"{anneal_factor(gen, generations, schedule):.3f}")
 
     if save_video:
-        from . import api
-        f0 = api.fitness(pop, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only)
-        save_frame_png(0, pop[int(np.argmin(f0))], pad, prefix, video_dir, H, W, k_sigma, None,
+        f0 = api.fitness(pop, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only,
+                         device=device)
+        save_frame_png(0, pop[int(np.argmin(f0))], pad, prefix, video_dir, H, W, k_sigma, device,
                        save_video)
     replay = getattr(draws, "generations", None) if draws is not None else None
     try:
@@ -473,8 +495,8 @@ def _genetic_approx_device(t, imp_mask, pop, H, W, generations, tour_k, elite_k,
                            mut_sigma_min=mut_sigma_min, schedule=schedule,
                            min_scale_splats=min_scale_splats, max_scale_splats=max_scale_splats,
                            k_sigma=k_sigma, boost_only=boost_only,
-                           seed=(int(np.random.SeedSequence().entropy) if seed is None else int(seed)) & (2**64 - 1), chunk=step, on_chunk=on_chunk,
-                           draws=replay)
+                           seed=resolve_seed(seed) & (2**64 - 1), chunk=step, on_chunk=on_chunk,
+                           draws=replay, device=api.device_index(device))
     finally:
         if bar is not None:
             bar.close()

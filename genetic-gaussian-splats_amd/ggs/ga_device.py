@@ -239,7 +239,8 @@ class RecordingDraws:
 def run_device_ga(target, imp_mask, init_pop, generations: int, *, tour_k: int, elite_k: int,
                   cxpb: float, mutpb: float, mut_sigma_max, mut_sigma_min, schedule: str,
                   min_scale_splats: float, max_scale_splats: float, k_sigma: float,
-                  boost_only: bool, seed: int, chunk: int, on_chunk=None, draws=None):
+                  boost_only: bool, seed: int, chunk: int, on_chunk=None, draws=None,
+                  device: int = 0):
     """algorithm.py:85-155 for ``generations`` generations on one GPU.
 
     ``draws``: optional list of per-generation draw dicts (replay); otherwise the
@@ -249,7 +250,7 @@ def run_device_ga(target, imp_mask, init_pop, generations: int, *, tour_k: int, 
                   mutpb=mutpb, mut_sigma_max=mut_sigma_max, mut_sigma_min=mut_sigma_min,
                   schedule=schedule, min_scale_splats=min_scale_splats,
                   max_scale_splats=max_scale_splats, k_sigma=k_sigma, boost_only=boost_only,
-                  seed=seed)
+                  seed=seed, device=device)
     try:
         gen = 1
         try:

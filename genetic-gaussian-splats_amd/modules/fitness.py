@@ -2,7 +2,9 @@
 
 One libggs.so call per batch: encode + prep + raster + fused weighted-L2
 reduction + fixed-order float64 finalize; the candidate images never reach HBM.
-``tile`` and ``device`` are accepted and ignored (results are tile-invariant).
+``tile`` is accepted and ignored (results are tile-invariant); ``device``
+selects the GPU as the reference's does ('cuda:k' → device k; 'cuda' / None →
+the launcher's LOCAL_RANK, else 0) — host arrays never fan out over every GPU.
 """
 from __future__ import annotations
 
@@ -38,7 +40,7 @@ def fitness_many(pop_batch, target, H: int, W: int, k_sigma: float, device, tile
     G = pop_batch if not isinstance(pop_batch, (list, tuple)) else \
         np.stack([ggs.as_f32(p) for p in pop_batch], 0)
     out = ggs.fitness(G, target, H, W, k_sigma, weight_mask=weight_mask,
-                      boost_only=boost_only, boost_beta=boost_beta)
+                      boost_only=boost_only, boost_beta=boost_beta, device=device)
     ref = first(pop_batch) if isinstance(pop_batch, (list, tuple)) else pop_batch
     return like(out, ref) if is_torch(ref) else out
 
@@ -55,4 +57,4 @@ def fitness_population(population, target, H: int, W: int, k_sigma: float, devic
                                     tile, weight_mask, boost_only).tolist())
         return out
     return ggs.fitness_population(population, target, H, W, k_sigma, chunk=chunk,
-                                  weight_mask=weight_mask, boost_only=boost_only)
+                                  weight_mask=weight_mask, boost_only=boost_only, device=device)

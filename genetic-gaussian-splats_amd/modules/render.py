@@ -4,8 +4,11 @@
 libggs.so (HIP, gfx950): prep + order-preserving per-tile cull + front-to-back
 blend, one launch each.  ``tile``, ``num_warps`` and ``num_stages`` are accepted
 and ignored — the reference output is tile-invariant and the
-MI355X kernel picks its own tiling.  ``use_fp16_canvas`` (never used by any
-reference caller) is accepted; the canvas is always float32.
+MI355X kernel picks its own tiling.  ``device`` selects the GPU as in the
+reference ('cuda:k' → device k; 'cuda' / None → the launcher's LOCAL_RANK, else
+0).  ``use_fp16_canvas`` (render.py:213, never set by a reference caller) keeps
+the reference's float16-canvas semantics: background and the stored pixels
+rounded to half precision (render.py:234-237), the blend in fp32.
 """
 from __future__ import annotations
 
@@ -33,8 +36,10 @@ def render_splats_rgb_triton(genomes, H: int, W: int, *, k_sigma: float = 3.0, d
         if C < 9:
             raise ggs.GGSInputError("Expected at least 9 genome cols")    # render.py:223
         out = torch.empty((B, H, W, 3), dtype=torch.float32, device=g.device)
+        bg = torch.tensor(background, dtype=torch.float16 if use_fp16_canvas else torch.float32)
         ggs.render_device(dev, stream_of(dev), g.data_ptr(), B, N, C, H, W, k_sigma,
-                          out.data_ptr(), background=background)
-        return out
-    out = ggs.render(genomes, H, W, k_sigma=k_sigma, background=background)
+                          out.data_ptr(), background=bg.float().tolist())
+        return out.half().float() if use_fp16_canvas else out
+    out = ggs.render(genomes, H, W, k_sigma=k_sigma, background=background, device=device,
+                     fp16_canvas=use_fp16_canvas)
     return like(out, genomes)

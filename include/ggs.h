@@ -164,7 +164,9 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
                   const float* mask_hw, const float* init_pop, void** handle);
 /* Shard the device GA's fitness evaluation over the ranks of `comm` (one
  * process per GPU; every rank created its session with the same config, target,
- * mask, initial population and seed, and steps it with the same arguments):
+ * mask, initial population and seed, and steps it with the same arguments —
+ * checked: the ranks exchange a 64-bit fingerprint of those inputs and the call
+ * fails with GGS_EINVAL on every rank if any differ):
  * each generation every rank breeds all P offspring (same draws), rasterises its
  * contiguous block of ceil(P/nranks), and one in-place RCCL all-gather of the
  * offspring fitness scalars lets every rank run the same survivors step, so the
@@ -227,6 +229,16 @@ int ggs_comm_allgather(void* comm, void* stream, const float* d_send, float* d_r
 int ggs_comm_wait(void* comm, void* stream, int64_t ticket);
 int ggs_comm_size(void* comm, int32_t* nranks, int32_t* rank);
 void ggs_comm_destroy(void* comm);
+/* Single-process communicators over the n listed devices (ncclCommInitAll; no id
+ * exchange): comms[i] is rank i on devices[i].  The host API uses this for its
+ * own multi-device fan-out (ggs_fitness with n_devices > 1). */
+int ggs_comm_init_local(int32_t n, const int32_t* devices, void** comms);
+/* Host-pointer all-gather (synchronous): recv[r*count + i] = rank r's send[i].
+ * Staged through the communicator's own device buffer and stream; for small
+ * control values (timings, session fingerprints).  count = 0: a barrier. */
+int ggs_comm_allgather_host(void* comm, const float* send, float* recv, int64_t count);
+/* Returns once every rank of `comm` has called it (host-side barrier). */
+int ggs_comm_barrier(void* comm);
 
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------
  * When enabled, every launch of "prep", "raster" and "finalize" is bracketed

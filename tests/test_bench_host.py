@@ -41,3 +41,86 @@ def test_pmc_figures_come_from_this_workloads_profile():
     assert traffic > 0 and src.startswith("profiles/r") and src.endswith("summary.json")
     busy = bench.pmc_valu_busy()
     assert 0.3 < busy < 1.0
+
+
+# ---- --gpus N: the rank spawn (no GPU: a stand-in script records what it got) ----
+_FAKE_RANK = r'''
+import json, os, sys
+out = sys.argv[sys.argv.index("--out") + 1]
+keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+        "GGS_RDZV_KEY")
+with open(os.path.join(out, "rank%s.json" % os.environ["RANK"]), "w") as f:
+    json.dump({k: os.environ.get(k) for k in keys} | {"argv": sys.argv[1:]}, f)
+fail = os.environ.get("FAKE_FAIL_RANK")
+sys.exit(3 if fail is not None and fail == os.environ["RANK"] else 0)
+'''
+
+
+def _fake(tmp_path):
+    p = tmp_path / "fake_rank.py"
+    p.write_text(_FAKE_RANK)
+    return str(p)
+
+
+def test_gpus_flag_spawns_one_process_per_rank(tmp_path):
+    import json
+    script = _fake(tmp_path)
+    rc = bench.spawn_ranks(4, ["--gpus", "4", "--steps", "7", "--out", str(tmp_path)],
+                           script=script, gpus_visible=8)
+    assert rc == 0
+    seen = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(4)]
+    assert [s["RANK"] for s in seen] == ["0", "1", "2", "3"]
+    assert [s["LOCAL_RANK"] for s in seen] == ["0", "1", "2", "3"]
+    assert {s["WORLD_SIZE"] for s in seen} == {"4"} and {s["MASTER_ADDR"] for s in seen} == {"127.0.0.1"}
+    assert len({s["MASTER_PORT"] for s in seen}) == 1 and len({s["GGS_RDZV_KEY"] for s in seen}) == 1
+    assert all(s["argv"][:4] == ["--gpus", "4", "--steps", "7"] for s in seen)
+
+
+def test_gpus_flag_failing_rank_fails_the_job(tmp_path, monkeypatch):
+    monkeypatch.setenv("FAKE_FAIL_RANK", "1")
+    rc = bench.spawn_ranks(2, ["--out", str(tmp_path)], script=_fake(tmp_path), gpus_visible=2)
+    assert rc == 3
+
+
+def test_gpus_flag_more_than_visible_fails_loudly(tmp_path, capsys):
+    rc = bench.spawn_ranks(8, ["--out", str(tmp_path)], script=_fake(tmp_path), gpus_visible=1)
+    assert rc == 2 and "only 1 GPU" in capsys.readouterr().err
+    assert not list(tmp_path.glob("rank*.json"))
+
+
+def test_gpus_flag_reaches_the_spawn(monkeypatch):
+    import pytest
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    got = {}
+    monkeypatch.setattr(bench, "spawn_ranks", lambda n, argv, **kw: got.update(n=n, argv=argv) or 0)
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "8", "--steps", "5"])
+    assert e.value.code == 0 and got == {"n": 8, "argv": ["--gpus", "8", "--steps", "5"]}
+
+
+def test_gpus_flag_must_match_the_launchers_world(monkeypatch):
+    import pytest
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "1"])
+    assert "WORLD_SIZE=2" in str(e.value.code)
+
+
+def test_strong_scaling_config_splits_the_population():
+    H, N, B, scaling = bench.CONFIGS["1024x8"]
+    assert (H, N, B, scaling) == (1024, 1024, 4096, "strong")       # BASELINE.json configs[3]
+    assert bench.CONFIGS["512"][:3] == (512, 256, 128)               # configs[1]
+    assert bench.CONFIGS["1024"][:3] == (1024, 1024, 512)            # configs[2]
+
+
+def test_visible_gpus_honours_visible_devices_lists(monkeypatch):
+    n = bench.visible_gpus()
+    if n is None:
+        return                                     # no KFD topology here (CPU container)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert bench.visible_gpus() == min(n, 1)
+
+
+def test_cpu_cores_respects_the_job_share(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench.cpu_cores() == min(3, len(os.sched_getaffinity(0)))

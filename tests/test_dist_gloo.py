@@ -71,4 +71,8 @@ def test_shard_bounds_cover_and_balance():
             assert spans[0][0] == 0 and spans[-1][1] == B
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             sizes = [b - a for a, b in spans]
-            assert max(sizes) - min(sizes) <= 1
+            per = -(-B // world)
+            # equal ceil(B/world) slots (one in-place all-gather), only the tail short
+            assert all(s == per for s in sizes[:B // per if per else 0])
+            assert all(0 <= s <= per for s in sizes)
+            assert all(a[0] == min(B, r * per) for r, a in enumerate(spans))

@@ -1,84 +1,140 @@
-"""The multi-GPU data-path collective through the C ABI:
-``ggs_comm_*`` all-gathers per-rank fitness scalars over RCCL on a HIP stream,
-in-stream or overlapped on the communicator's own stream.  One GPU here, so a
-world-1 communicator (rank 0's id carried over a gloo process group, as
-``ggs.RcclGather`` does at any world size); the N > 1 sharding logic is covered
-on CPU by tests/test_dist_gloo.py and run at N = 2..8 by bench.py.
+"""The multi-GPU data-path collective through the C ABI, with no
+PyTorch: ``ggs_comm_*`` all-gathers per-rank fitness scalars over RCCL on a HIP
+stream (in-stream or overlapped on the communicator's own stream), the
+single-process communicators of the host API's fan-out (``ggs_comm_init_local``),
+and the host-side barrier / all-gather.  One GPU here, so world-1 communicators;
+the N > 1 sharding logic and the file rendezvous are covered on CPU
+(tests/test_dist_gloo.py, tests/test_host_semantics.py) and run at N = 2..8 by
+bench.py.
 """
 from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 
 import ggs
 import ggs_oracle as O
+from conftest import ORACLE, PKG
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def world1():
-    import socket
-
-    import torch.distributed as dist
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
-    yield
-    dist.destroy_process_group()
+def hip():
+    from ggs import hip as h
+    ggs.ensure_init()
+    h.set_device(0)
+    return h
 
 
 @pytest.mark.parametrize("overlap", [False, True])
-def test_rccl_allgather_returns_every_shard(world1, overlap):
-    import torch
-    dev = torch.device("cuda", 0)
-    comm = ggs.RcclGather(0)
-    st = torch.cuda.current_stream(dev).cuda_stream
+def test_rccl_allgather_returns_every_shard(hip, overlap, monkeypatch):
+    monkeypatch.setenv("GGS_COMM_RCCL_SELF", "1")      # world 1: through RCCL, not the copy kernel
+    comm = ggs.RcclGather(0, rank=0, world=1)
+    st = hip.Stream()
     try:
         for count in (1, 128, 4099):
-            send = torch.arange(count, dtype=torch.float32, device=dev) * 0.5 - 3.0
-            recv = torch.full((count * comm.world,), float("nan"), device=dev)
-            t = comm.allgather(st, send.data_ptr(), recv.data_ptr(), count, overlap=overlap)
+            x = (np.arange(count, dtype=np.float32) * 0.5 - 3.0)
+            send = hip.DeviceArray.from_host(x)
+            recv = hip.DeviceArray.from_host(np.full(count * comm.world, np.nan, np.float32))
+            t = comm.allgather(st.handle, send.ptr, recv.ptr, count, overlap=overlap)
             assert (t >= 0) == overlap
-            comm.wait(st, t)
-            torch.cuda.synchronize(dev)
-            assert torch.equal(recv[comm.rank * count:(comm.rank + 1) * count], send)
+            comm.wait(st.handle, t)
+            np.testing.assert_array_equal(recv.to_host(st)[comm.rank * count:(comm.rank + 1) * count], x)
     finally:
         comm.close()
 
 
-def test_sharded_fitness_through_rccl_matches_oracle(world1):
+def test_host_allgather_and_barrier(hip):
+    comm = ggs.RcclGather(0, rank=0, world=1)
+    try:
+        v = np.array([1.5, -2.0, 3.25], np.float32)
+        got = comm.allgather_host(v)
+        assert got.shape == (1, 3)
+        np.testing.assert_array_equal(got[0], v)
+        # bit patterns survive (fingerprints travel as float32 pairs)
+        raw = np.array([0x7FC00001, 0xFFFFFFFF], np.uint32).view(np.float32)
+        assert comm.allgather_host(raw).view(np.uint32).tolist() == [[0x7FC00001, 0xFFFFFFFF]]
+        comm.barrier()
+    finally:
+        comm.close()
+
+
+def test_sharded_fitness_through_rccl_matches_oracle(hip):
     """bench.py's step: fused fitness of this rank's candidates into a ring slot,
     overlapped gather, join — the gathered vector equals the oracle's fitness."""
-    import torch
-    dev = torch.device("cuda", 0)
     H = W = 64
     B, N = 6, 12
     pop = O.synthetic_population(B, N, H, W, seed=7)
     rng = np.random.default_rng(3)
     tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
     mask = rng.uniform(0.4, 1.0, (H, W)).astype(np.float32)
-    g = torch.from_numpy(pop).to(dev)
-    t_d, m_d = torch.from_numpy(tgt).to(dev), torch.from_numpy(mask).to(dev)
-    out = torch.empty(B, device=dev)
-    st = torch.cuda.current_stream(dev).cuda_stream
-    comm = ggs.RcclGather(0)
+    g, t_d, m_d = (hip.DeviceArray.from_host(a) for a in (pop, tgt, mask))
+    out = hip.DeviceArray((B,))
+    st = hip.Stream()
+    comm = ggs.RcclGather(0, rank=0, world=1)
     try:
-        plan = ggs.TargetPlan(0, st, t_d.data_ptr(), m_d.data_ptr(), ggs.GGS_FIT_WEIGHTED, 1.0, H, W)
-        plan.fitness_device(st, g.data_ptr(), B, N, 9, 3.0, out.data_ptr())
-        full = torch.empty(B * comm.world, device=dev)
-        comm.wait(st, comm.allgather(st, out.data_ptr(), full.data_ptr(), B, overlap=True))
-        got = full.cpu().numpy()[:B]
+        plan = ggs.TargetPlan(0, st.handle, t_d.ptr, m_d.ptr, ggs.GGS_FIT_WEIGHTED, 1.0, H, W)
+        plan.fitness_device(st.handle, g.ptr, B, N, 9, 3.0, out.ptr)
+        full = hip.DeviceArray((B * comm.world,))
+        comm.wait(st.handle, comm.allgather(st.handle, out.ptr, full.ptr, B, overlap=True))
+        got = full.to_host(st)[:B]
     finally:
         comm.close()
     ref = np.asarray(O.fitness_many(list(pop), tgt, H, W, 3.0, weight_mask=mask))
     assert np.max(np.abs(got - ref) / np.abs(ref)) <= 1e-5
 
 
+def test_local_communicators(hip):
+    """ggs_comm_init_local (ncclCommInitAll): one rank per listed device."""
+    devs = (C.c_int32 * 1)(0)
+    comms = (C.c_void_p * 1)()
+    ggs._lib.check(ggs.lib.ggs_comm_init_local(1, devs, comms), "ggs_comm_init_local")
+    n, r = C.c_int32(), C.c_int32()
+    ggs._lib.check(ggs.lib.ggs_comm_size(comms[0], C.byref(n), C.byref(r)), "ggs_comm_size")
+    assert (n.value, r.value) == (1, 0)
+    ggs._lib.check(ggs.lib.ggs_comm_barrier(comms[0]), "ggs_comm_barrier")
+    ggs.lib.ggs_comm_destroy(comms[0])
+    bad = (C.c_int32 * 2)(0, 0)
+    out2 = (C.c_void_p * 2)()
+    with pytest.raises(ggs.GGSInputError):
+        ggs._lib.check(ggs.lib.ggs_comm_init_local(2, bad, out2), "ggs_comm_init_local")
+
+
+_FANOUT = r'''
+import sys, numpy as np
+sys.path[:0] = [{pkg!r}, {oracle!r}]
+import ggs, ggs_oracle as O
+H, W = 96, 80
+pop = O.synthetic_population(37, 20, H, W, seed=4)
+rng = np.random.default_rng(8)
+tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+mask = rng.uniform(0.4, 1.0, (H, W)).astype(np.float32)
+got = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask, n_devices=0)
+np.save(sys.argv[1], got)
+'''
+
+
+def test_host_fanout_gathers_through_rccl(tmp_path):
+    """The host API's multi-device fan-out returns the scalars with ONE RCCL
+    all-gather + one D2H (north_star); GGS_FANOUT_RCCL=1 takes that path at one
+    device: identical to the plain call, bit for bit."""
+    script = _FANOUT.format(pkg=PKG, oracle=ORACLE)
+    outs = []
+    for force in ("0", "1"):
+        path = str(tmp_path / f"fit{force}.npy")
+        env = dict(os.environ, GGS_FANOUT_RCCL=force)
+        subprocess.run([sys.executable, "-c", script, path], env=env, check=True, timeout=120)
+        outs.append(np.load(path))
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
 def test_comm_argument_errors():
-    import ctypes as C
     h = C.c_void_p()
     idb = (C.c_uint8 * 128)()
     with pytest.raises(ggs.GGSInputError):
@@ -88,11 +144,12 @@ def test_comm_argument_errors():
 
 
 @pytest.mark.parametrize("via", ["copy", "rccl"])
-def test_device_ga_sharded_over_world1_comm_is_the_plain_ga(world1, via, monkeypatch):
+def test_device_ga_sharded_over_world1_comm_is_the_plain_ga(hip, via, monkeypatch):
     """ggs_ga_set_comm: breed all, evaluate this rank's shard, all-gather the
     fitness scalars — at world 1 the whole generation, bit-identical to the
     unsharded session (populations, fitness, best, curves).  "rccl" routes the
-    single-rank gather through RCCL's in-place all-gather instead of the copy."""
+    single-rank gather through RCCL's in-place all-gather instead of the copy.
+    set_comm also exchanges the sessions' fingerprints (here: with itself)."""
     if via == "rccl":
         monkeypatch.setenv("GGS_COMM_RCCL_SELF", "1")
     from ggs import ga
@@ -109,7 +166,7 @@ def test_device_ga_sharded_over_world1_comm_is_the_plain_ga(world1, via, monkeyp
     res = []
     for shard in (False, True):
         d = DeviceGA(tgt, mask, init, **cfg)
-        comm = ggs.RcclGather(0) if shard else None
+        comm = ggs.RcclGather(0, rank=0, world=1) if shard else None
         if shard:
             d.set_comm(comm)
         d.run(1, 12, 12)
