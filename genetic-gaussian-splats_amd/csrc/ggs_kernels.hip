@@ -78,35 +78,20 @@ prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, f
 // ---------------------------------------------------------------------------
 // raster
 // ---------------------------------------------------------------------------
-#ifndef GGS_ROWS
-#define GGS_ROWS 128              // strip height: 32 pixels per lane (tools/ablate.py: 64 rows
-#endif                            // at 5 waves/SIMD 0.260 ms, 96 at 4: 0.249, 128 at 3: 0.249)
 constexpr int TILE = 64;          // tile width (pixels): 4 strips of 16 columns
-constexpr int TILE_H = GGS_ROWS;  // tile height (rows); one wave covers a 16 x TILE_H strip
+constexpr int TILE_H = 128;       // tile height: one wave covers a 16 x 128 strip, 32 pixels per lane
+                                  // (round 1: 64 rows at 5 waves/SIMD 0.260 ms, 96 at 4: 0.249, 128 at 3: 0.249)
 constexpr int RG = TILE_H / 4;    // row groups per lane (rows r, r+4, ...)
 constexpr int NPK = RG / 2;       // packed row-group pairs per lane
-#ifndef GGS_WPB
-#define GGS_WPB 1
-#endif
-constexpr int WPB = GGS_WPB;      // waves per workgroup (each wave owns one 16-column strip)
+constexpr int WPB = 1;            // one wave per workgroup, one 16-column strip each (2 or 4 waves:
+                                  // +1.4 %, +2.5 % raster time, round 1)
 constexpr int NT = 64 * WPB;      // threads per workgroup
 constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
-#ifndef GGS_XCD_SPREAD
-#define GGS_XCD_SPREAD 1          // spread each candidate's strips over the XCDs
-#endif
-#ifndef GGS_PK_EPI
-#define GGS_PK_EPI 1              // fitness epilogue colours by v_pk_fma_f32 ... clamp (inline asm;
-#endif                            // bit-identical to the scalar v_fma clamp path, ~1 % faster)
-#ifndef GGS_CULL_PF
-#define GGS_CULL_PF 1             // cull bounds loads in flight (chunks of 64 splats)
-#endif
-#ifndef GGS_PREFETCH
-#define GGS_PREFETCH 2            // next record loaded while the current one is blended (2: two alternating register sets)
-#endif
-#ifndef GGS_OCC
-#define GGS_OCC 3                 // waves per SIMD the register budget is sized for (158 VGPRs)
-#endif
+constexpr int OCC = 3;            // waves per SIMD the register budget is sized for (<= 168 VGPRs)
+// candidate rotation across the XCDs advances every 2^XCD_SHIFT strip groups (see the grid order)
+constexpr int XCD_SHIFT = 3;
+constexpr int CULL_PRIO = 2;      // s_setprio while culling (1 and 3 measured the same)
 
 // Saturation cut-off.  Front to back, a strip's pixels receive Σ_rest T·f·c +
 // T_end·bg ≤ T from all the splats still to come (Σ w + T_end = T, c, bg ≤ 1).
@@ -160,49 +145,18 @@ __device__ __forceinline__ float keep_if(uint64_t lanes, float f) {
     return __builtin_amdgcn_inverse_ballot_w64(lanes) ? f : 0.0f;
 }
 
-#define GGS_FOR16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
-// One (splat, row group) pair for this lane's pixel (col, ty0 + 4g + ph):
-// e = K*quad + log2(a) (see make_rec), f = 2^e, front-to-back "over":
+// Two adjacent row groups (2k, 2k+1) per lane live in one float2, so qy, the
+// quadratic and the blend run as v_pk_{add,fma,mul}_f32 (2 FP32 ops per lane per
+// issue); the exp stays per element.  e = K*quad + log2(a) (see make_rec),
+// f = 2^e, front-to-back "over":
 //   C += T*f*c ; T *= (1 - f)       (== render.py:194-196 run back-to-front)
-// MASKED adds the per-lane row test for the AABB's first/last row block.
-// Performance-ablation switch (tools/ablate.py; 0 in every shipped build):
-// 1 = exp replaced by a multiply, 2 = no row-group bodies, 3 = red channel only,
-// 4 = cull + epilogue only (no per-splat work), 5 = no epilogue, 6 = dispatch only,
-// 7 = every wave reads one of 8 candidates' records (record-cache locality probe).
-#ifndef GGS_ABL
-#define GGS_ABL 0
-#endif
-#if GGS_ABL == 1
-#define GGS_EXP2(x) ((x) * 0.0001f)
-#else
 #define GGS_EXP2(x) __builtin_amdgcn_exp2f(x)
-#endif
-#define GGS_PAIR(g, MASKED)                                                        \
-    do {                                                                           \
-        if (GGS_ABL == 2) break;                                                   \
-        const float qy_ = qy0 + (float)(4 * (g));                                  \
-        float e_ = __builtin_fmaf(qy_, __builtin_fmaf(Cc, qy_, bx), px);           \
-        if (MASKED && (unsigned)(4 * (g) - rlo) > rspan) e_ = -__builtin_inff();   \
-        const float w_ = T##g * GGS_EXP2(e_);                                      \
-        R##g = __builtin_fmaf(w_, cr, R##g);                                       \
-        if (GGS_ABL != 3) G##g = __builtin_fmaf(w_, cg, G##g);                     \
-        if (GGS_ABL != 3) Bl##g = __builtin_fmaf(w_, cb, Bl##g);                   \
-        T##g = T##g - w_;                                                          \
-    } while (0)
-
-// Packed variant (GGS_PACKED): two adjacent row groups (2k, 2k+1) per lane in
-// one float2, so qy / the quadratic / the blend run as v_pk_{add,fma,mul}_f32
-// (2 FP32 ops per lane per issue); the exp stays per element.
-#ifndef GGS_PACKED
-#define GGS_PACKED 1
-#endif
-static_assert(NPK <= 16 && (GGS_PACKED || RG <= 16), "walk macros cover 16 pairs / 16 groups");
+static_assert(NPK <= 16, "walk macros cover 16 pairs");
 typedef float f2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_elementwise_fma(a, b, c); }
 #define GGS_PK(k, MASKED)                                                            \
     do {                                                                             \
-        if (GGS_ABL == 2) break;                                                     \
         const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                   \
         f2_t e_ = fma2(qy_, fma2((f2_t)s.Cc, qy_, bx2), px2);                               \
         if (MASKED) {                                                                \
@@ -213,19 +167,18 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
         f_.x = GGS_EXP2(e_.x);                                                       \
         f_.y = GGS_EXP2(e_.y);                                                       \
         const f2_t w_ = P_T##k * f_;                                                 \
-        P_R##k = fma2((f2_t)s.r, w_, P_R##k);                                              \
-        if (GGS_ABL != 3) P_G##k = fma2((f2_t)s.g, w_, P_G##k);                            \
-        if (GGS_ABL != 3) P_B##k = fma2((f2_t)s.b, w_, P_B##k);                            \
+        P_R##k = fma2((f2_t)s.r, w_, P_R##k);                                        \
+        P_G##k = fma2((f2_t)s.g, w_, P_G##k);                                        \
+        P_B##k = fma2((f2_t)s.b, w_, P_B##k);                                        \
         P_T##k = P_T##k - w_;                                                        \
     } while (0)
 // Blend one packed pair with given (row-masked) Gaussian values f.
 #define GGS_BLEND(k, F)                                                              \
     do {                                                                             \
-        if (GGS_ABL == 2) break;                                                     \
         const f2_t w_ = P_T##k * (F);                                                \
-        P_R##k = fma2((f2_t)s.r, w_, P_R##k);                                              \
-        if (GGS_ABL != 3) P_G##k = fma2((f2_t)s.g, w_, P_G##k);                            \
-        if (GGS_ABL != 3) P_B##k = fma2((f2_t)s.b, w_, P_B##k);                            \
+        P_R##k = fma2((f2_t)s.r, w_, P_R##k);                                        \
+        P_G##k = fma2((f2_t)s.g, w_, P_G##k);                                        \
+        P_B##k = fma2((f2_t)s.b, w_, P_B##k);                                        \
         P_T##k = P_T##k - w_;                                                        \
     } while (0)
 #define GGS_BLEND_REC(k)                                                             \
@@ -239,24 +192,20 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 
 // MODE: 0 = write image, 1 = fitness (weights from the target plan)
 //
-// One wave per workgroup (GGS_WPB); wave w of a 64 x TILE_H tile owns the
+// One wave per workgroup (WPB); wave w of a 64 x TILE_H tile owns the
 // 16-column strip [tx0+16w, tx0+16w+15] x TILE_H rows.  No workgroup barrier
 // anywhere: each wave culls the candidate's splats against its own strip (64
 // per step, highest index first, ballot + mbcnt compaction -> an order-
 // preserving LDS list), blends that list front-to-back, and writes its own
 // partial sum.  TILE_H = 128: 128 accumulator VGPRs (+~35) -> 3 waves per SIMD.
 template <int MODE, bool SAT>
-__global__ void __launch_bounds__(NT, GGS_OCC)
+__global__ void __launch_bounds__(NT, OCC)
 raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
               const float* __restrict__ clean) {
     __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
-    if (GGS_ABL == 6) {               // ablation: dispatch only
-        if (threadIdx.x == 0 && partials) partials[blockIdx.x] = 0.0f;
-        return;
-    }
 
     const int lane = threadIdx.x & 63;
 #if GGS_TIMING
@@ -269,21 +218,14 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     // candidate; groups go central (heavy) first to shorten the grid's tail
     const int gi = blockIdx.x / B;
     const int grp = tile_order ? tile_order[gi] : gi;
-#if GGS_XCD_SPREAD
     // candidates rotate by one per group: with B % 8 == 0 a fixed b would stay on
     // one XCD (blocks go round-robin to the 8 XCDs) and per-XCD work would be the
     // sum of 16 candidates' costs (tools/probe/wave_timing.py: XCD end times 197-207 us)
-    // ... but only every 2^GGS_XCD_SHIFT groups: blocks B apart (the next group's
+    // ... but only every 2^XCD_SHIFT groups: blocks B apart (the next group's
     // block in the same XCD slot) then run the same candidate, whose records stay
     // in that XCD's caches across 8 groups (raster -0.5 %, one stream +0.7 %;
     // shifts 2-5 measured alike, 0 = rotate every group)
-#ifndef GGS_XCD_SHIFT
-#define GGS_XCD_SHIFT 3
-#endif
-    const int b = (int)((blockIdx.x + (gi >> GGS_XCD_SHIFT)) % B);
-#else
-    const int b = blockIdx.x % B;
-#endif
+    const int b = (int)((blockIdx.x + (gi >> XCD_SHIFT)) % B);
     const int t = grp / SPB;
     const int wv = (grp % SPB) * WPB + wib;           // strip 0..3 of the tile
     const int tx0 = (t % nTX) * TILE;
@@ -305,59 +247,35 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 
     // 16 pixels per lane x (R, G, B, transmittance), as named scalars: arrays
     // get vectorised into <16 x float> values whose phis the allocator splits.
-#if GGS_PACKED
 #define GGS_DECL(k) f2_t P_R##k = 0.0f, P_G##k = 0.0f, P_B##k = 0.0f, P_T##k = 1.0f;
     GGS_FOR16P(GGS_DECL)
-#else
-#define GGS_DECL(g) float R##g = 0.0f, G##g = 0.0f, Bl##g = 0.0f, T##g = 1.0f;
-    GGS_FOR16(GGS_DECL)
-#endif
 #undef GGS_DECL
 
-    const SplatRec* __restrict__ crec = recs + (GGS_ABL == 7 ? (int64_t)(b & 7) : (int64_t)b) * N;   // ABL 7: 8 shared candidates
+    const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
     int* __restrict__ list = &lists[0][0] + wib * CAP;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
 
-    // bounds of the next 64 splats are loaded GGS_CULL_PF chunks ahead (the
-    // cull does little work per chunk, so it waits on these loads)
+    // bounds of the next 64 splats are loaded one chunk ahead (the cull does
+    // little work per chunk, so it waits on these loads; two chunks ahead: no gain)
     auto bounds = [&](int i) { return *reinterpret_cast<const int4*>(&crec[max(i, 0)].x0); };
     int4 bbn = bounds(N - 1 - lane);
-#if GGS_CULL_PF >= 2
-    int4 bbn2 = bounds(N - 1 - 64 - lane);
-#endif
-#if GGS_CULL_PF >= 4
-    int4 bbn3 = bounds(N - 1 - 128 - lane), bbn4 = bounds(N - 1 - 192 - lane);
-#endif
-#ifndef GGS_CULL_PRIO
-#define GGS_CULL_PRIO 2              // 1 and 3 measured the same
-#endif
-#ifndef GGS_PRIO
-#define GGS_PRIO 1          // wave priority: culls (load-bound) ahead of blends; +0.4 %
-#endif
     for (int base = 0; base < N; base += 64) {
-        if (GGS_PRIO == 1) __builtin_amdgcn_s_setprio(GGS_CULL_PRIO);   // cull: loads issue first
+        // wave priority: the load-bound cull issues ahead of other waves' blends (+0.4 %)
+        __builtin_amdgcn_s_setprio(CULL_PRIO);
         // --- cull 64 splats (descending index = front-to-back) against the strip:
         // one 16-B load per lane (clamped index, no short-circuit: a branchy test
         // splits it into two dependent loads), then a branch-free overlap test
         const int i = N - 1 - (base + lane);
         const int4 bb = bbn;                                                  // x0 x1 y0 y1
-#if GGS_CULL_PF >= 4
-        bbn = bbn2; bbn2 = bbn3; bbn3 = bbn4; bbn4 = bounds(i - 256);
-#elif GGS_CULL_PF >= 2
-        bbn = bbn2; bbn2 = bounds(i - 128);
-#else
         bbn = bounds(i - 64);
-#endif
         const bool hit = (i >= 0) & (bb.w >= ty0) & (bb.z <= ty1) & (bb.y >= sx0) & (bb.x <= sx0 + 15);
         const uint64_t m = __ballot(hit);
         if (hit) list[cnt + __popcll(m & lt_mask)] = i * (int)sizeof(SplatRec);   // byte offset
         cnt += __popcll(m);
         if (cnt <= CAP - 64 && base + 64 < N) continue;
         if (cnt == 0) continue;
-        if (GGS_ABL == 4) { asm volatile("" :: "v"(list[lane])); cnt = 0; continue; }
-        if (GGS_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-        if (GGS_PRIO == 2) __builtin_amdgcn_s_setprio(1);   // blend ahead of other waves' culls
+        __builtin_amdgcn_s_setprio(0);
 #if GGS_TIMING
         { GGS_TMARK(now); t_cull += now - t_mark; t_mark = now; n_vis += cnt; }
 #endif
@@ -376,7 +294,6 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             const int dy0 = y0 - ty0, dy1 = y1 - ty0;          // AABB rows relative to the tile
             const int gA = max(dy0, 0) >> 2;                   // first / last row group
             const int gB = min(dy1, TILE_H - 1) >> 2;
-            [[maybe_unused]] const float Cc = s.Cc, cr = s.r, cg = s.g, cb = s.b;   // unpacked walk
             const float qx = Xf - s.cx;
             const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
             const float px = inx ? __builtin_fmaf(s.A * qx, qx, s.la) : -__builtin_inff();
@@ -385,7 +302,6 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             const int rlo = y0 - ty0 - ph;                     // row test: 4g - rlo in [0, rspan]
             const unsigned rspan = (unsigned)(y1 - y0);
 
-#if GGS_PACKED
             const f2_t qyv = {qy0, qy0 + 4.0f}, bx2 = bx, px2 = px;
             const int kA = gA >> 1, kB = gB >> 1;             // first / last group pair
             f2_t F2, R2;                                       // row recurrence: f, ratio
@@ -519,44 +435,8 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 #undef GGS_LAST
                 default: __builtin_unreachable();
             }
-#else
-            // Duff's-device walk over the row groups gA..gB: the first and last
-            // group masked per lane, the ones in between unmasked, 2 scalar ops
-            // per group (needs -simplifycfg-sink-common=false, see Makefile).
-            switch (gA) {
-#define GGS_FIRST(g) \
-    case g: if (g < RG) { GGS_PAIR(g, true); if (gB == g) goto done; goto u##g; } break;
-                GGS_FIRST(0) GGS_FIRST(1) GGS_FIRST(2) GGS_FIRST(3) GGS_FIRST(4)
-                GGS_FIRST(5) GGS_FIRST(6) GGS_FIRST(7) GGS_FIRST(8) GGS_FIRST(9)
-                GGS_FIRST(10) GGS_FIRST(11) GGS_FIRST(12) GGS_FIRST(13) GGS_FIRST(14)
-                GGS_FIRST(15)
-#undef GGS_FIRST
-                default: __builtin_unreachable();
-            }
-#define GGS_MID(gp, g) u##gp: if (gB == g) goto last; if (g < RG) GGS_PAIR(g, false);
-            GGS_MID(0, 1) GGS_MID(1, 2) GGS_MID(2, 3) GGS_MID(3, 4) GGS_MID(4, 5)
-            GGS_MID(5, 6) GGS_MID(6, 7) GGS_MID(7, 8) GGS_MID(8, 9) GGS_MID(9, 10)
-            GGS_MID(10, 11) GGS_MID(11, 12) GGS_MID(12, 13) GGS_MID(13, 14)
-            GGS_MID(14, 15)
-#undef GGS_MID
-        u15:
-        last:
-            switch (gB) {
-#define GGS_LAST(g) case g: if (g < RG) GGS_PAIR(g, true); break;
-                GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
-                GGS_LAST(7) GGS_LAST(8) GGS_LAST(9) GGS_LAST(10) GGS_LAST(11) GGS_LAST(12)
-                GGS_LAST(13) GGS_LAST(14) GGS_LAST(15)
-#undef GGS_LAST
-                default: __builtin_unreachable();
-            }
-#endif
         done:;
-#if GGS_ABL == 2
-            asm volatile("" :: "v"(px), "v"(bx), "v"(qy0), "v"(rlo), "s"(rspan), "s"(Cc), "s"(cr),
-                         "s"(cg), "s"(cb), "s"(gA), "s"(gB));
-#endif
         };
-#if GGS_PREFETCH == 2
         // two records in alternating SGPR sets: the next record is loaded into
         // the set the finished visit used, so no register rotation at the latch
         auto load_at = [&](int jj) __attribute__((always_inline)) {
@@ -588,25 +468,6 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             }
 #endif
         }
-#elif GGS_PREFETCH
-        SplatRec nxt = *reinterpret_cast<const SplatRec*>(cbase + (unsigned)__builtin_amdgcn_readlane(offv, 0));
-        int jr = 63;                  // last j before the next 64 offsets are needed
-        for (int j = 0; j < cnt; ++j) {
-            const SplatRec s = nxt;
-            if (j == jr) {
-                jr += 64;
-                offv = list[min(j + 1 + lane, cnt - 1)];
-            }
-            nxt = *reinterpret_cast<const SplatRec*>(
-                cbase + (unsigned)__builtin_amdgcn_readlane(offv, (j + 1) & 63));   // waited at the latch
-            visit(s);
-        }
-#else
-        for (int j = 0; j < cnt; ++j) {
-            if (j > 0 && (j & 63) == 0) offv = list[min(j + lane, cnt - 1)];
-            visit(*reinterpret_cast<const SplatRec*>(cbase + (unsigned)__builtin_amdgcn_readlane(offv, j & 63)));
-        }
-#endif
         cnt = 0;
 #if GGS_TIMING
         { GGS_TMARK(now); t_vis += now - t_mark; t_mark = now; }
@@ -614,12 +475,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     }
 
     // --- epilogue ---------------------------------------------------------------
-    if (GGS_ABL == 5) {               // ablation: no epilogue
-        if (lane == 0 && MODE != 0) partials[((int64_t)b * nTiles + t) * 4 + wv] = (float)cnt;
-        return;
-    }
     float R[RG], G[RG], Bl[RG], T[RG];
-#if GGS_PACKED
 #define GGS_PACK(k)                                                                   \
     if (k < NPK) {                                                                    \
         R[2 * k] = P_R##k.x; G[2 * k] = P_G##k.x; Bl[2 * k] = P_B##k.x; T[2 * k] = P_T##k.x; \
@@ -627,10 +483,6 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         T[2 * k + 1] = P_T##k.y;                                                      \
     }
     GGS_FOR16P(GGS_PACK)
-#else
-#define GGS_PACK(g) if (g < RG) { R[g] = R##g; G[g] = G##g; Bl[g] = Bl##g; T[g] = T##g; }
-    GGS_FOR16(GGS_PACK)
-#endif
 #undef GGS_PACK
     if (MODE == 0) {
         if (col < W) {
@@ -653,16 +505,13 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
         // lines up with the packed accumulators (two pixels per v_pk op).
         const float4* __restrict__ P = plan + (int64_t)(t * 4 + wv) * RG * 64 + lane;
         f2_t accp = 0.0f;
-#if GGS_PK_EPI
         // background pairs (bg, bg) in SGPR pairs: no VGPRs at the epilogue's peak
         const uint64_t bg2r = (uint64_t)__float_as_uint(bg_r) * 0x100000001ull;
         const uint64_t bg2g = (uint64_t)__float_as_uint(bg_g) * 0x100000001ull;
         const uint64_t bg2b = (uint64_t)__float_as_uint(bg_b) * 0x100000001ull;
-#endif
 #pragma unroll
         for (int k = 0; k < NPK; ++k) {
             const float4 qa = P[(2 * k) * 64], qb = P[(2 * k + 1) * 64];
-#if GGS_PK_EPI
             // packed: one v_pk_fma_f32 with the clamp bit per channel and row pair
             // (the compiler folds the clamp only into the scalar v_fma_f32)
             const f2_t T2 = {T[2 * k], T[2 * k + 1]};
@@ -670,15 +519,6 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
             asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(c_r) : "v"(T2), "s"(bg2r), "v"((f2_t){R[2 * k], R[2 * k + 1]}));
             asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(c_g) : "v"(T2), "s"(bg2g), "v"((f2_t){G[2 * k], G[2 * k + 1]}));
             asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(c_b) : "v"(T2), "s"(bg2b), "v"((f2_t){Bl[2 * k], Bl[2 * k + 1]}));
-#else
-            f2_t c_r, c_g, c_b;       // clamp folds into the scalar v_fma (clamp bit)
-            c_r.x = fminf(fmaxf(__builtin_fmaf(T[2 * k], bg_r, R[2 * k]), 0.0f), 1.0f);
-            c_r.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_r, R[2 * k + 1]), 0.0f), 1.0f);
-            c_g.x = fminf(fmaxf(__builtin_fmaf(T[2 * k], bg_g, G[2 * k]), 0.0f), 1.0f);
-            c_g.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_g, G[2 * k + 1]), 0.0f), 1.0f);
-            c_b.x = fminf(fmaxf(__builtin_fmaf(T[2 * k], bg_b, Bl[2 * k]), 0.0f), 1.0f);
-            c_b.y = fminf(fmaxf(__builtin_fmaf(T[2 * k + 1], bg_b, Bl[2 * k + 1]), 0.0f), 1.0f);
-#endif
             const f2_t dr = c_r - (f2_t){qa.x, qa.y};
             const f2_t dg = c_g - (f2_t){qa.z, qa.w};
             const f2_t db = c_b - (f2_t){qb.x, qb.y};
@@ -705,7 +545,6 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     }
 #endif
 }
-#undef GGS_PAIR
 
 // ---------------------------------------------------------------------------
 // target plan: the fitness epilogue's inputs re-laid out in raster lane order
