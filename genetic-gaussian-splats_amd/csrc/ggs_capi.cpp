@@ -1028,16 +1028,20 @@ struct SaSession {
     bool incremental = false;   // measured slower at every SA config tried
     DevBuf curr, best, nb, nb_fits, target, mask, draws;
     DevBuf cur_recs, nb_recs, cur_part, nb_part, dirty, plan, wpart, order, counters;
+    DevBuf loop, sit, curves;       // device SA loop (ggs_sa_run): state, per-iteration table, curves
     float* h_fits = nullptr;        // pinned
     unsigned* h_counters = nullptr; // pinned: [0] changed splats (last propose)
+    SaLoopDev* h_loop = nullptr;    // pinned copy of the loop state
     uint64_t n_changed = 0, n_proposed = 0;
+    int driver = 0;                 // 1: ggs_sa_propose/commit, 2: ggs_sa_run (not mixed)
 };
 
 void sa_free(SaSession* s) {
     for (DevBuf* b : {&s->curr, &s->best, &s->nb, &s->nb_fits, &s->target, &s->mask, &s->draws,
                       &s->cur_recs, &s->nb_recs, &s->cur_part, &s->nb_part, &s->dirty, &s->plan,
-                      &s->wpart, &s->order, &s->counters})
+                      &s->wpart, &s->order, &s->counters, &s->loop, &s->sit, &s->curves})
         if (b->p) (void)hipFree(b->p);
+    if (s->h_loop) (void)hipHostFree(s->h_loop);
     if (s->h_fits) (void)hipHostFree(s->h_fits);
     if (s->h_counters) (void)hipHostFree(s->h_counters);
     if (s->st) (void)hipStreamDestroy(s->st);
@@ -1295,10 +1299,11 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
         (rc = ensure(s->dirty, slots * s->cap, s->st)) || (rc = ensure(s->plan, plan_bytes(cfg->H, cfg->W), s->st)) ||
         (rc = ensure(s->wpart, sizeof(float) * slots, s->st)) ||
         (rc = ensure(s->order, sizeof(int) * (size_t)raster_order_len(cfg->H, cfg->W), s->st)) ||
-        (rc = ensure(s->counters, sizeof(unsigned) * 4, s->st)))
+        (rc = ensure(s->counters, sizeof(unsigned) * 4, s->st)) || (rc = ensure(s->loop, sizeof(SaLoopDev), s->st)))
         return bail(rc);
     if (hipHostMalloc((void**)&s->h_fits, sizeof(float) * s->cap, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&s->h_counters, sizeof(unsigned) * 4, hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc((void**)&s->h_counters, sizeof(unsigned) * 4, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&s->h_loop, sizeof(SaLoopDev), hipHostMallocDefault) != hipSuccess)
         return bail(fail(GGS_ENOMEM, "pinned allocation failed"));
     std::vector<int> order(raster_order_len(cfg->H, cfg->W));
     raster_tile_order(cfg->H, cfg->W, order.data());
@@ -1320,6 +1325,12 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
         hipStreamSynchronize(s->st))
         return bail(fail(GGS_EHIP, "initial evaluation failed"));
     if (init_fit) *init_fit = s->h_fits[0];
+    // the device loop's state: current = best = the initial energy, no acceptances yet
+    *s->h_loop = SaLoopDev{};
+    s->h_loop->acc_j = -1;
+    s->h_loop->curr_fit = s->h_loop->best_fit = (double)s->h_fits[0];
+    if (hipMemcpy(s->loop.p, s->h_loop, sizeof(SaLoopDev), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(GGS_EHIP, "upload failed"));
     *handle = s.release();
     return GGS_OK;
 }
@@ -1330,7 +1341,9 @@ int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_
     SaSession* s = (SaSession*)handle;
     if (n < 1 || n > s->cap) return fail(GGS_EINVAL, "n=%d outside [1, %d]", n, s->cap);
     if (first_try < 0) return fail(GGS_EINVAL, "first_try must be >= 0");
+    if (s->driver == 2) return fail(GGS_EINVAL, "this SA session is driven by ggs_sa_run");
     std::lock_guard<std::mutex> lk(s->c->mu);
+    s->driver = 1;
     DeviceGuard dg(s->c->dev);
     GaDrawsDev d{};
     int rc;
@@ -1368,6 +1381,7 @@ int ggs_sa_commit(void* handle, int32_t j, int32_t update_best) {
     if (!handle) return fail(GGS_EINVAL, "null handle");
     SaSession* s = (SaSession*)handle;
     if (j >= s->last_n) return fail(GGS_EINVAL, "neighbour %d not proposed (last n=%d)", j, s->last_n);
+    if (s->driver == 2) return fail(GGS_EINVAL, "this SA session is driven by ggs_sa_run");
     std::lock_guard<std::mutex> lk(s->c->mu);
     DeviceGuard dg(s->c->dev);
     const size_t ib = sizeof(float) * 9 * (size_t)s->N;
@@ -1380,6 +1394,126 @@ int ggs_sa_commit(void* handle, int32_t j, int32_t update_best) {
                                s->st));
     }
     if (update_best) GGS_HIP(hipMemcpyAsync(s->best.p, s->curr.p, ib, hipMemcpyDeviceToDevice, s->st));
+    return GGS_OK;
+}
+
+int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iters, int32_t tries,
+               const double* temps, int32_t width, double* curves_out) {
+    if (!handle) return fail(GGS_EINVAL, "null handle");
+    SaSession* s = (SaSession*)handle;
+    if (first_it < 0 || n_its < 0 || tries < 1) return fail(GGS_EINVAL, "need first_it >= 0, n_its >= 0, tries >= 1");
+    if (n_its > 0 && (!temps || !curves_out)) return fail(GGS_EINVAL, "null temps / curves");
+    if (width < 0 || width > s->cap) return fail(GGS_EINVAL, "width=%d outside [0, %d]", width, s->cap);
+    if ((int64_t)(first_it + (int64_t)n_its) * tries > INT32_MAX)
+        return fail(GGS_EINVAL, "iterations x tries must stay below 2^31");
+    if (s->driver == 1) return fail(GGS_EINVAL, "this SA session is driven by ggs_sa_propose/commit");
+    if (n_its == 0) return GGS_OK;
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    DeviceGuard dg(s->c->dev);
+    s->driver = 2;
+    const ggs_ga_config& c = s->cfg;
+    std::vector<SaItDev> tab((size_t)n_its);
+    for (int i = 0; i < n_its; ++i) {
+        const GaParamsDev q = ga_params(c, first_it + i, total_iters);
+        tab[i] = SaItDev{{q.sig_xy, q.sig_alog, q.sig_blog, q.sig_theta, q.sig_rgb, q.sig_alpha}, {0.f, 0.f},
+                         temps[i]};
+    }
+    int rc;
+    if ((rc = ensure(s->sit, sizeof(SaItDev) * (size_t)n_its, s->st)) ||
+        (rc = ensure(s->curves, sizeof(double) * 2 * (size_t)n_its, s->st)))
+        return rc;
+    SaLoopDev* loop = (SaLoopDev*)s->loop.p;
+    const SaItDev* sit = (const SaItDev*)s->sit.p;
+    double* curves = (double*)s->curves.p;
+    GGS_HIP(hipMemcpyAsync(s->sit.p, tab.data(), sizeof(SaItDev) * (size_t)n_its, hipMemcpyHostToDevice, s->st));
+    const int64_t pos0 = (int64_t)first_it * tries, end = pos0 + (int64_t)n_its * tries;
+    GGS_HIP(launch_sa_begin(s->st, loop, pos0, end, tries, first_it, s->cap, width));
+    GaParamsDev prm = ga_params(c, first_it, total_iters);   // sigmas replaced per neighbour from sit
+    prm.mutate_only = 1;
+    prm.o_base = 0;
+    const bool fuse_prep = s->N <= 1024 || s->cap >= 64;     // as ggs_sa_propose
+    const int nslots = 4 * s->nTiles;
+    const float bg[3] = {1.f, 1.f, 1.f};
+    const int* live = &loop->live;
+    auto round = [&]() -> int {
+        {
+            ProfScope ps(s->st, 0);
+            GGS_HIP(launch_ga_variation(s->st, (const float*)s->curr.p, nullptr, 1, s->N, prm, GaDrawsDev{}, c.seed,
+                                        first_it, (float*)s->nb.p, s->cap,
+                                        fuse_prep ? (SplatRec*)s->nb_recs.p : nullptr, c.H, c.W, c.k_sigma, loop,
+                                        sit));
+            if (!fuse_prep)
+                GGS_HIP(launch_prep(s->st, true, (const float*)s->nb.p, (int64_t)s->cap * s->N, 9, c.H, c.W,
+                                    c.k_sigma, (SplatRec*)s->nb_recs.p, nullptr, nullptr, nullptr, live, s->N));
+        }
+        if (s->incremental)
+            GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, (const float*)s->nb.p,
+                                 (const SplatRec*)s->cur_recs.p, (const SplatRec*)s->nb_recs.p, s->cap, s->N, c.H,
+                                 c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p, live));
+        {
+            ProfScope ps(s->st, 1);
+            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->nb_recs.p, s->cap, s->N, c.H, c.W, bg, nullptr,
+                                  (const float4*)s->plan.p, (float*)s->nb_part.p, (const int*)s->order.p,
+                                  s->incremental ? (const unsigned char*)s->dirty.p : nullptr,
+                                  (const float*)s->cur_part.p, live));
+        }
+        {
+            ProfScope ps(s->st, 2);
+            GGS_HIP(launch_finalize(s->st, (const float*)s->nb_part.p, (const float*)s->wpart.p, s->cap, s->nTiles,
+                                    c.fitness_mode, c.H, c.W, (float*)s->nb_fits.p, live));
+        }
+        GGS_HIP(launch_sa_accept(s->st, loop, sit, (const float*)s->nb_fits.p, c.seed, curves, (float*)s->curr.p,
+                                 (float*)s->best.p, (const float*)s->nb.p, s->N,
+                                 s->incremental ? (SplatRec*)s->cur_recs.p : nullptr,
+                                 (const SplatRec*)s->nb_recs.p, (float*)s->cur_part.p,
+                                 (const float*)s->nb_part.p, nslots));
+        return GGS_OK;
+    };
+    // Rounds are enqueued in batches with one host sync between batches: a round
+    // consumes at most its width in tries, so ceil(remaining / width) rounds never
+    // overshoot the chunk (rounds past its end would be empty launches anyway).
+    const uint64_t evaluated0 = s->h_loop->evaluated;
+    int64_t remaining = end - pos0;
+    int est = width > 0 ? width : (s->h_loop->acc_rate < 1.0 / s->cap ? s->cap
+                                   : std::max(1, (int)lrint(1.0 / s->h_loop->acc_rate)));
+    for (;;) {
+        const int64_t R = std::max<int64_t>(1, (remaining + est - 1) / std::max(1, est));
+        for (int64_t r = 0; r < R; ++r)
+            if ((rc = round())) return rc;
+        GGS_HIP(hipMemcpyAsync(s->h_loop, loop, sizeof(SaLoopDev), hipMemcpyDeviceToHost, s->st));
+        GGS_HIP(hipStreamSynchronize(s->st));
+        if (s->h_loop->pos >= end) break;
+        remaining = end - s->h_loop->pos;
+        est = std::max(1, (int)s->h_loop->live);
+    }
+    GGS_HIP(hipMemcpyAsync(curves_out, curves, sizeof(double) * 2 * (size_t)n_its, hipMemcpyDeviceToHost, s->st));
+    if (s->incremental) {
+        GGS_HIP(hipMemcpyAsync(s->h_counters, s->counters.p, sizeof(unsigned), hipMemcpyDeviceToHost, s->st));
+        GGS_HIP(hipMemsetAsync(s->counters.p, 0, sizeof(unsigned), s->st));
+    }
+    GGS_HIP(hipStreamSynchronize(s->st));
+    if (s->incremental) s->n_changed += s->h_counters[0];
+    s->n_proposed += s->h_loop->evaluated - evaluated0;
+    return GGS_OK;
+}
+
+int ggs_sa_loop_state(void* handle, double* best_fit, double* curr_fit, uint64_t* rounds, uint64_t* evaluated,
+                      uint64_t* accepted) {
+    if (!handle) return fail(GGS_EINVAL, "null handle");
+    SaSession* s = (SaSession*)handle;
+    std::lock_guard<std::mutex> lk(s->c->mu);
+    const SaLoopDev& l = *s->h_loop;     // as of the end of the last ggs_sa_run (or creation)
+    if (best_fit) *best_fit = l.best_fit;
+    if (curr_fit) *curr_fit = l.curr_fit;
+    if (rounds) *rounds = l.rounds;
+    if (evaluated) *evaluated = l.evaluated;
+    if (accepted) *accepted = l.accepted;
+    return GGS_OK;
+}
+
+int ggs_sa_accept_uniform(uint64_t seed, int32_t it, int32_t k, double* u) {
+    if (!u || it < 0 || k < 0) return fail(GGS_EINVAL, "bad arguments");
+    *u = sa_accept_uniform(seed, (uint32_t)it, (uint32_t)k);
     return GGS_OK;
 }
 

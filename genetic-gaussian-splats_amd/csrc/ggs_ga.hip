@@ -30,7 +30,7 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
-__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+__host__ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
@@ -44,7 +44,16 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
 // stream ids: which draw a 4-word Philox block feeds
-enum : uint32_t { S_MASK = 1, S_NORM_A = 2, S_NORM_B = 3, S_NORM_C = 4, S_IND = 5, S_TOUR = 6, S_CX = 7 };
+enum : uint32_t { S_MASK = 1, S_NORM_A = 2, S_NORM_B = 3, S_NORM_C = 4, S_IND = 5, S_TOUR = 6, S_CX = 7,
+                  S_ACCEPT = 8 };
+
+// SA acceptance uniform of try (it, k): 53 bits of one Philox block -> [0, 1)
+// (the role of random.random() at annealing.py:140-142).  Host and device.
+__host__ __device__ __forceinline__ double accept_u(uint64_t seed, uint32_t it, uint32_t k) {
+    const U4 r = philox({it, k, 0u, S_ACCEPT}, (uint32_t)seed, (uint32_t)(seed >> 32));
+    return ((double)(r.x >> 5) * 67108864.0 + (double)(r.y >> 6)) * (1.0 / 9007199254740992.0);
+}
+double sa_accept_uniform(uint64_t seed, uint32_t it, uint32_t k) { return accept_u(seed, it, k); }
 
 struct Rng {
     uint32_t k0, k1, gen;
@@ -101,7 +110,8 @@ template <int VT>
 __global__ void __launch_bounds__(VT)
 ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fits, int P, int N,
                     GaParamsDev prm, GaDrawsDev d, uint32_t k0, uint32_t k1, int gen,
-                    float* __restrict__ off, SplatRec* __restrict__ recs, int H, int W, float k_sigma) {
+                    float* __restrict__ off, SplatRec* __restrict__ recs, int H, int W, float k_sigma,
+                    const SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit) {
     __shared__ int s_a, s_b, s_cx;
     __shared__ float s_sizei;
     __shared__ int s_j, s_count;
@@ -110,9 +120,19 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
     const int pair = o >> 1;
     const bool first = (o & 1) == 0;
     const int tid = threadIdx.x;
-    const Rng rng{k0, k1, (uint32_t)gen};
 
-    const uint32_t og = (uint32_t)(o + prm.o_base);   // Philox identity of this offspring
+    uint32_t og = (uint32_t)(o + prm.o_base);   // Philox identity of this offspring
+    if (sl) {   // SA loop round: neighbour o is global try pos + o = (it, k); it's sigmas from sit
+        if (o >= sl->live) return;
+        const int64_t g = sl->pos + o;
+        const int it = (int)(g / sl->tries);
+        og = (uint32_t)(g % sl->tries);
+        gen = it;
+        const SaItDev& q = sit[it - sl->first_it];
+        prm.sig_xy = q.sig[0]; prm.sig_alog = q.sig[1]; prm.sig_blog = q.sig[2];
+        prm.sig_theta = q.sig[3]; prm.sig_rgb = q.sig[4]; prm.sig_alpha = q.sig[5];
+    }
+    const Rng rng{k0, k1, (uint32_t)gen};
     if (tid == 0 && prm.mutate_only) {
         s_a = 0;                               // annealing.py:122-128: mutate the current state
         s_b = 0;
@@ -482,13 +502,14 @@ ga_gather_kernel(const float* __restrict__ pop, const float* __restrict__ off, i
 // ---------------------------------------------------------------------------
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
-                               float* off, int n_off, SplatRec* recs, int H, int W, float k_sigma) {
+                               float* off, int n_off, SplatRec* recs, int H, int W, float k_sigma,
+                               const SaLoopDev* sl, const SaItDev* sit) {
     if (n_off < 64 && N >= 1024)
         hipLaunchKernelGGL(ga_variation_kernel<1024>, dim3(n_off), dim3(1024), 0, st, pop, fits, P, N, prm, d,
-                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma);
+                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma, sl, sit);
     else
         hipLaunchKernelGGL(ga_variation_kernel<256>, dim3(n_off), dim3(256), 0, st, pop, fits, P, N, prm, d,
-                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma);
+                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma, sl, sit);
     return hipGetLastError();
 }
 
@@ -510,5 +531,115 @@ hipError_t launch_ga_gather(hipStream_t st, const float* pop, const float* off, 
 }
 
 int ga_max_population() { return SMAX; }
+
+// ---------------------------------------------------------------------------
+// device SA loop (ggs_sa_run): chunk start, and one round's acceptance walk
+// ---------------------------------------------------------------------------
+// Round width: the host loop's rule (ggs/annealing.py) without its iteration
+// boundary — 1/acceptance rate, or the capacity while acceptances are rarer than that.
+__device__ __forceinline__ int sa_width(const SaLoopDev& s) {
+    int w = s.width;
+    if (w <= 0) w = s.acc_rate < 1.0 / s.cap ? s.cap : max(1, (int)rint(1.0 / s.acc_rate));
+    w = min(w, s.cap);
+    return (int)min((int64_t)w, max(s.end - s.pos, (int64_t)0));
+}
+
+__global__ void sa_begin_kernel(SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it, int cap,
+                                int width) {
+    sl->pos = pos;
+    sl->end = end;
+    sl->tries = tries;
+    sl->first_it = first_it;
+    sl->cap = cap;
+    sl->width = width;
+    sl->acc_j = -1;
+    sl->new_best = 0;
+    sl->live = sa_width(*sl);
+}
+
+// annealing.py:130-150 over the round's neighbours, in try order, by one thread;
+// then the workgroup installs the accepted neighbour.  Same arithmetic as the
+// host loop (ggs/annealing.py): dE in float64 from the float32 energies, the
+// Metropolis test u < exp(-dE/T) (device exp; the host's math.exp agrees to the
+// last ulp in all but rare cases, and u would have to fall between the two),
+// the 1e-12 best margin.
+__global__ void __launch_bounds__(256)
+sa_accept_kernel(SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, const float* __restrict__ fits,
+                 uint64_t seed, double* __restrict__ curves, float* __restrict__ curr, float* __restrict__ best,
+                 const float* __restrict__ nb, int N, SplatRec* __restrict__ cur_recs,
+                 const SplatRec* __restrict__ nb_recs, float* __restrict__ cur_part,
+                 const float* __restrict__ nb_part, int nslots) {
+    __shared__ int s_j, s_nb;
+    if (threadIdx.x == 0) {
+        SaLoopDev s = *sl;
+        int jacc = -1, nbest = 0;
+        if (s.live > 0) {
+            int used = s.live;
+            for (int j = 0; j < s.live; ++j) {
+                const int64_t g = s.pos + j;
+                const int it = (int)(g / s.tries), k = (int)(g % s.tries);
+                const double T = sit[it - s.first_it].T;
+                const double e_new = (double)fits[j];
+                const double dE = e_new - s.curr_fit;                       // annealing.py:133
+                bool acc = dE <= 0.0;
+                if (!acc && T > 0.0) acc = accept_u(seed, (uint32_t)it, (uint32_t)k) < exp(-dE / T);
+                s.acc_rate = 0.9 * s.acc_rate + 0.1 * (acc ? 1.0 : 0.0);
+                if (acc) s.curr_fit = e_new;
+                const bool nbst = s.curr_fit + 1e-12 < s.best_fit;            // annealing.py:148-150
+                if (nbst) s.best_fit = s.curr_fit;
+                if (k == s.tries - 1) {                                     // end of iteration `it`
+                    curves[2 * (int64_t)(it - s.first_it)] = s.best_fit;
+                    curves[2 * (int64_t)(it - s.first_it) + 1] = s.curr_fit;
+                }
+                if (acc) {          // the later tries were mutated from the old state
+                    jacc = j;
+                    nbest = nbst;
+                    used = j + 1;
+                    s.accepted += 1;
+                    break;
+                }
+            }
+            s.evaluated += (uint64_t)s.live;
+            s.rounds += 1;
+            s.pos += used;
+        }
+        s.acc_j = jacc;
+        s.new_best = nbest;
+        s.live = sa_width(s);
+        *sl = s;
+        s_j = jacc;
+        s_nb = nbest;
+    }
+    __syncthreads();
+    const int j = s_j;
+    if (j < 0) return;
+    const int64_t n9 = (int64_t)N * 9;
+    const float* src = nb + j * n9;
+    for (int64_t i = threadIdx.x; i < n9; i += blockDim.x) {
+        const float v = src[i];
+        curr[i] = v;
+        if (s_nb) best[i] = v;
+    }
+    if (cur_recs) {         // incremental evaluation keeps the state's records and partials
+        const float4* rs = reinterpret_cast<const float4*>(nb_recs + j * (int64_t)N);
+        float4* rd = reinterpret_cast<float4*>(cur_recs);
+        for (int64_t i = threadIdx.x; i < 4 * (int64_t)N; i += blockDim.x) rd[i] = rs[i];
+        for (int i = threadIdx.x; i < nslots; i += blockDim.x) cur_part[i] = nb_part[(int64_t)j * nslots + i];
+    }
+}
+
+hipError_t launch_sa_begin(hipStream_t st, SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it,
+                           int cap, int width) {
+    hipLaunchKernelGGL(sa_begin_kernel, dim3(1), dim3(1), 0, st, sl, pos, end, tries, first_it, cap, width);
+    return hipGetLastError();
+}
+
+hipError_t launch_sa_accept(hipStream_t st, SaLoopDev* sl, const SaItDev* sit, const float* fits, uint64_t seed,
+                            double* curves, float* curr, float* best, const float* nb, int N, SplatRec* cur_recs,
+                            const SplatRec* nb_recs, float* cur_part, const float* nb_part, int nslots) {
+    hipLaunchKernelGGL(sa_accept_kernel, dim3(1), dim3(256), 0, st, sl, sit, fits, seed, curves, curr, best, nb,
+                       N, cur_recs, nb_recs, cur_part, nb_part, nslots);
+    return hipGetLastError();
+}
 
 }  // namespace ggs

@@ -23,18 +23,22 @@ struct __attribute__((aligned(16))) SplatRec {
 };
 static_assert(sizeof(SplatRec) == 64, "SplatRec must be 64 bytes");
 
+// live (device, may be null): only the first *live candidates of N splats each are
+// live (the device SA loop sizes its grids for the session's capacity and sets the
+// round's neighbour count on the device); the other threads / waves exit at once.
 hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_t S, int C, int H,
-                       int W, float k, SplatRec* recs, float* f9, int* i4, float* enc9);
+                       int W, float k, SplatRec* recs, float* f9, int* i4, float* enc9,
+                       const int* live = nullptr, int n_per = 0);
 int raster_tiles(int H, int W, int* nTX);
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty = nullptr,
-                         const float* clean = nullptr);
+                         const float* clean = nullptr, const int* live = nullptr);
 // Strips touched by splats that differ between `nb` [n][N][9] and `curr` [N][9]
 // (old AABB from cur_recs, new from nb_recs) -> dirty [n][tiles][4] (zeroed first).
 hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, const SplatRec* cur_recs,
                         const SplatRec* nb_recs, int n, int N, int H, int W, unsigned char* dirty,
-                        unsigned* n_changed);
+                        unsigned* n_changed, const int* live = nullptr);
 // Target plan for the fitness epilogue (built once per target/mask/mode/beta).
 hipError_t launch_plan(hipStream_t st, const float* target, const float* mask, int mode, float beta,
                        int H, int W, float4* plan, float* wpartials);
@@ -47,7 +51,7 @@ int raster_order_len(int H, int W);
 hipError_t launch_detmath(hipStream_t st, const float* x, const float* y, int64_t n, int fn,
                           float* out);
 hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,
-                           int nTiles, int mode, int H, int W, float* out);
+                           int nTiles, int mode, int H, int W, float* out, const int* live = nullptr);
 
 // ---- device GA (ggs_ga.hip) -------------------------------------------------
 struct GaParamsDev {            // one generation's operator parameters (float32 as the host path)
@@ -78,11 +82,52 @@ struct GaBestDev {
     int* updated;
     float* ind;                 // [N*9]
 };
+// ---- device SA loop (ggs_sa_run) ---------------------------------------------
+// Tries are numbered globally, g = it * tries + k.  A round mutates the next
+// `live` tries from the current state (Philox keyed by (seed, it, k), as
+// ggs_sa_propose), evaluates them, and the accept kernel walks them in order
+// (annealing.py:133-150): the first acceptance installs that neighbour and ends
+// the round (the later tries came from the old state and are re-proposed by the
+// next round); without one the round consumes all `live` tries.
+struct SaLoopDev {
+    int64_t pos, end;           // next try / one past the chunk's last try
+    int32_t live;               // neighbours of the current round (0: chunk done)
+    int32_t acc_j;              // neighbour the last round accepted (-1: none)
+    int32_t new_best;           // ... and whether it became the best
+    int32_t tries, first_it;    // tries per iteration; iteration of sit[0]
+    int32_t cap, width;         // neighbour capacity; fixed width (0: adaptive)
+    int32_t pad_;
+    double acc_rate;            // EWMA of acceptances per try (ggs/annealing.py)
+    double best_fit;
+    double curr_fit;            // float32 energy of the current state, widened
+    uint64_t evaluated, rounds, accepted;
+};
+struct SaItDev {                // one iteration of the chunk
+    float sig[6];               // build_mut_sigma at this iteration
+    float pad_[2];
+    double T;                   // temperature (annealing.py:29-44)
+};
+// One device round's acceptance walk + install of the accepted neighbour
+// (genome; records and strip partials too when `recs_too`, for the incremental
+// path); curves[(it - first_it)*2 + {0,1}] = best, current after each iteration.
+hipError_t launch_sa_accept(hipStream_t st, SaLoopDev* sl, const SaItDev* sit, const float* fits, uint64_t seed,
+                            double* curves, float* curr, float* best, const float* nb, int N, SplatRec* cur_recs,
+                            const SplatRec* nb_recs, float* cur_part, const float* nb_part, int nslots);
+// Start a chunk: pos/end/tries/first_it, and the first round's width.
+hipError_t launch_sa_begin(hipStream_t st, SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it,
+                           int cap, int width);
+// The acceptance uniform of try (it, k): Philox4x32-10 keyed by seed, 53-bit double
+// in [0, 1).  Host and device compute the same bits.
+double sa_accept_uniform(uint64_t seed, uint32_t it, uint32_t k);
+
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
                                float* off, int n_off,    // n_off offspring (GA: P; SA: tries)
-                               SplatRec* recs = nullptr, int H = 0, int W = 0, float k_sigma = 3.0f);
-                               // recs != null: also prep the offspring (records [n_off][N])
+                               SplatRec* recs = nullptr, int H = 0, int W = 0, float k_sigma = 3.0f,
+                               const SaLoopDev* sl = nullptr, const SaItDev* sit = nullptr);
+                               // recs != null: also prep the offspring (records [n_off][N]);
+                               // sl != null: SA loop round (neighbour o = try sl->pos + o, its
+                               // iteration's sigmas from sit; o >= sl->live exits)
 struct FitReduce {               // survivors reduces the offspring's strip partials itself
     const float* partials = nullptr; // [P][nT] (null: use off_fits)
     const float* wpartials = nullptr;

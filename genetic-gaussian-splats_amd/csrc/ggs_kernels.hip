@@ -48,9 +48,10 @@ template <bool ENCODE>
 __global__ void __launch_bounds__(256)
 prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, float k,
             SplatRec* __restrict__ recs, float* __restrict__ f9, int* __restrict__ i4,
-            float* __restrict__ enc9) {
+            float* __restrict__ enc9, const int* __restrict__ live, int n_per) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= S) return;
+    if (live && i >= (int64_t)*live * n_per) return;   // SA loop: candidates past the round's count
     const float* g = genomes + i * (int64_t)C;
     float row[9];
     if (ENCODE) {
@@ -204,7 +205,7 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
-              const float* __restrict__ clean) {
+              const float* __restrict__ clean, const int* __restrict__ live) {
     __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
 
     const int lane = threadIdx.x & 63;
@@ -214,6 +215,13 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
     unsigned n_vis = 0;
 #endif
     const int wib = ufirst((int)(threadIdx.x >> 6));  // wave in block (uniform: keeps control on SALU)
+    // SA loop rounds: the grid is sized for the session's capacity and only the
+    // first *live candidates are evaluated; the grid order below is then that of
+    // a launch over *live candidates, and the blocks past it exit at once
+    if (live) {
+        B = ufirst(*live);
+        if ((int64_t)blockIdx.x >= (int64_t)B * nTiles * SPB) return;
+    }
     // strip-major grid: B consecutive blocks run one strip (group) for every
     // candidate; groups go central (heavy) first to shorten the grid's tail
     const int gi = blockIdx.x / B;
@@ -612,9 +620,10 @@ __device__ __forceinline__ void mark_strips(const SplatRec& r, int nTX, unsigned
 __global__ void __launch_bounds__(256)
 dirty_kernel(const float* __restrict__ curr, const float* __restrict__ nb,
              const SplatRec* __restrict__ cur_recs, const SplatRec* __restrict__ nb_recs, int n, int N,
-             int nTX, int nTiles, unsigned char* __restrict__ dirty, unsigned* __restrict__ n_changed) {
+             int nTX, int nTiles, unsigned char* __restrict__ dirty, unsigned* __restrict__ n_changed,
+             const int* __restrict__ live) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)n * N) return;
+    if (idx >= (int64_t)(live ? min(*live, n) : n) * N) return;
     const int b = (int)(idx / N), i = (int)(idx % N);
     const unsigned* a = reinterpret_cast<const unsigned*>(curr + (int64_t)i * 9);
     const unsigned* c = reinterpret_cast<const unsigned*>(nb + idx * 9);
@@ -630,7 +639,7 @@ dirty_kernel(const float* __restrict__ curr, const float* __restrict__ nb,
 
 hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, const SplatRec* cur_recs,
                         const SplatRec* nb_recs, int n, int N, int H, int W, unsigned char* dirty,
-                        unsigned* n_changed) {
+                        unsigned* n_changed, const int* live) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     hipError_t e = hipMemsetAsync(dirty, 0, (size_t)n * nTiles * 4, st);
@@ -638,7 +647,7 @@ hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, cons
     const int64_t tot = (int64_t)n * N;
     if (tot == 0) return hipSuccess;
     hipLaunchKernelGGL(dirty_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, curr, nb,
-                       cur_recs, nb_recs, n, N, nTX, nTiles, dirty, n_changed);
+                       cur_recs, nb_recs, n, N, nTX, nTiles, dirty, n_changed, live);
     return hipGetLastError();
 }
 
@@ -649,9 +658,9 @@ size_t plan_bytes(int H, int W) { return sizeof(float4) * 4 * (size_t)raster_til
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 finalize_kernel(const float* __restrict__ partials, const float* __restrict__ wpartials,
-                int nTiles, int mode, double hw, int B, float* __restrict__ out) {
+                int nTiles, int mode, double hw, int B, float* __restrict__ out, const int* __restrict__ live) {
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per candidate (ggs_prep.h)
-    if (b >= B) return;
+    if (b >= B || (live && b >= *live)) return;
     const float v = finalize_wave(partials, wpartials, nTiles, mode, hw, b);
     if ((threadIdx.x & 63) == 0) out[b] = v;
 }
@@ -689,15 +698,16 @@ hipError_t launch_detmath(hipStream_t st, const float* x, const float* y, int64_
 // launchers (called from ggs_capi.cpp; no allocation, no sync)
 // ---------------------------------------------------------------------------
 hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_t S, int C, int H,
-                       int W, float k, SplatRec* recs, float* f9, int* i4, float* enc9) {
+                       int W, float k, SplatRec* recs, float* f9, int* i4, float* enc9, const int* live,
+                       int n_per) {
     if (S <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((S + 255) / 256);
     if (encode)
         hipLaunchKernelGGL(prep_kernel<true>, dim3(grid), dim3(256), 0, st, genomes, S, C, H, W, k,
-                           recs, f9, i4, enc9);
+                           recs, f9, i4, enc9, live, n_per);
     else
         hipLaunchKernelGGL(prep_kernel<false>, dim3(grid), dim3(256), 0, st, genomes, S, C, H, W, k,
-                           recs, f9, i4, enc9);
+                           recs, f9, i4, enc9, live, n_per);
     return hipGetLastError();
 }
 
@@ -730,13 +740,14 @@ int raster_tiles(int H, int W, int* nTX) {
 
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
-                         const int* tile_order, const unsigned char* dirty, const float* clean) {
+                         const int* tile_order, const unsigned char* dirty, const float* clean,
+                         const int* live) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
 #define GGS_RASTER(M, S)                                                                       \
     hipLaunchKernelGGL((raster_kernel<M, S>), grid, block, 0, st, recs, B, N, H, W, nTX, nTiles, \
-                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean)
+                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live)
     // the saturation check only where strip lists can grow long (N > SAT_MIN_SPLATS);
     // at the bench's 256 splats the kernel without it is the faster code (+1.6 %)
     const bool sat = N > SAT_MIN_SPLATS;
@@ -747,10 +758,10 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, 
 }
 
 hipError_t launch_finalize(hipStream_t st, const float* partials, const float* wpartials, int B,
-                           int nTiles, int mode, int H, int W, float* out) {
+                           int nTiles, int mode, int H, int W, float* out, const int* live) {
     // 4 strip partials per (candidate, tile)
     hipLaunchKernelGGL(finalize_kernel, dim3((B + 3) / 4), dim3(256), 0, st, partials, wpartials, nTiles * 4,
-                       mode, (double)H * (double)W, B, out);
+                       mode, (double)H * (double)W, B, out, live);
     return hipGetLastError();
 }
 

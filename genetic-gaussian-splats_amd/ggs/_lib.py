@@ -84,6 +84,12 @@ SIGNATURES = {
     "ggs_sa_destroy": (None, [C.c_void_p]),
     "ggs_sa_set_incremental": (C.c_int, [C.c_void_p, C.c_int32]),
     "ggs_sa_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "ggs_sa_run": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                             C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_double)]),
+    "ggs_sa_loop_state": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_uint64)]),
+    "ggs_sa_accept_uniform": (C.c_int, [C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_double)]),
     "ggs_comm_unique_id": (C.c_int, [C.c_void_p]),
     "ggs_comm_create": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
                                   C.POINTER(C.c_void_p)]),

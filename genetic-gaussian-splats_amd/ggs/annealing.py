@@ -17,6 +17,17 @@ individual and the curves are exactly the sequential loop's
 ``speculate`` bounds the batch width: None adapts it to the observed
 acceptance rate (wide when moves are rarely accepted — the common case at low
 temperature — narrow when most are).
+
+With the device backend and no explicit draws the loop itself runs on the GPU
+(``ggs_sa_run``, ``loop="device"``, the default there): a round mutates the next
+tries from the current state — across iteration boundaries, so a round can hold
+more neighbours than one iteration has tries when acceptances are rare —
+evaluates them in one launch, and a one-workgroup kernel walks them in order
+with the same Metropolis test and installs the accepted neighbour; the host
+syncs once per batch of rounds.  Its acceptance uniforms are Philox keyed by
+(seed, iteration, try) (``ga_device.PhiloxAcceptDraws``), so ``loop="host"``
+with the device backend replays the same trajectory on the host
+(tests/test_gpu_ga.py).
 """
 from __future__ import annotations
 
@@ -59,7 +70,8 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
                         evaluate: Optional[Callable[[np.ndarray], np.ndarray]] = None,
                         init_individual: Optional[np.ndarray] = None, progress: bool = True,
                         return_state: bool = False, speculate: Optional[int] = None,
-                        backend: str = "auto", incremental: bool = False):
+                        backend: str = "auto", incremental: bool = False, loop: str = "auto",
+                        chunk: int = 256):
     """annealing.py:47-190 → (best individual [N, 9] float32, best energy).
 
     Keyword-only hooks as ggs.ga.genetic_approx (``seed``, ``draws`` — a source
@@ -73,7 +85,11 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
     (bit-identical results; off by default — the double ``wrap_angle`` of
     genetic.py:71 + utils.py:43 moves many θ by an ulp on every mutation, so
     most strips are dirty anyway and the bookkeeping costs more than it saves,
-    DESIGN.md §9)."""
+    DESIGN.md §9).  ``loop``: "device" (the whole iteration on the GPU, see the
+    module doc; device backend, Philox draws), "host" (acceptance test in Python)
+    or "auto" (device when possible).  ``chunk``: iterations per ``ggs_sa_run``
+    call in the device loop (progress bar / interrupt granularity; video frames
+    fall on chunk ends)."""
     from .mask import compute_importance_mask, prepare_target
     from .ga import resolve_seed
     seed = resolve_seed(seed)                                # run_sags.py:26-27 seeds `random`
@@ -91,14 +107,28 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
             return api.fitness(G, t, H, W, k_sigma, weight_mask=imp_mask, boost_only=boost_only,
                                device=device)
     explicit = draws is not None
-    draws = draws if draws is not None else NumpyDraws(seed)
+    if loop == "auto":
+        loop = "device" if backend == "device" and not explicit else "host"
+    if loop not in ("host", "device"):
+        raise ValueError(f"loop must be 'auto', 'host' or 'device', got {loop!r}")
+    if loop == "device" and (backend != "device" or explicit):
+        raise ValueError("loop='device' needs backend='device' and the in-kernel (Philox) draws")
+    if draws is None:
+        if backend == "device":          # Philox mutation in-kernel; acceptance as ggs_sa_run
+            from .ga_device import PhiloxAcceptDraws
+            draws = PhiloxAcceptDraws(seed)
+        else:
+            draws = NumpyDraws(seed)
     curr = (np.array(init_individual, np.float32, copy=True) if init_individual is not None else
             new_population(1, n_splats, H, W, min_scale_splats, max_scale_splats,
                            np.random.default_rng(seed))[0])
     N = curr.shape[0]
     tries = max(0, int(tries_per_iter))
     if backend == "device":
-        prop = _DeviceProposer(t, imp_mask, curr, max(1, tries), mutpb, mut_sigma_max,
+        cap = max(1, tries)
+        if loop == "device":             # a round may span iterations: size it to fill the GPU
+            cap = max(1, int(speculate)) if speculate is not None else device_loop_width(H, W, tries)
+        prop = _DeviceProposer(t, imp_mask, curr, cap, mutpb, mut_sigma_max,
                                mut_sigma_min, sigma_schedule, min_scale_splats, max_scale_splats,
                                k_sigma, boost_only, seed, incremental, device)
     elif backend == "host":
@@ -114,6 +144,16 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
         if save_video:
             save_frame_png(0, prop.best(), pad, prefix, video_dir, H, W, k_sigma, device, save_video)
 
+        if loop == "device":
+            best_fit, curr_fit, stats = _device_loop(
+                prop.sa, curves, iterations, tries, sched, temp0, 0 if speculate is None else
+                max(1, int(speculate)), chunk, progress, save_video, frame_every,
+                lambda i: save_frame_png(i, prop.best(), pad, prefix, video_dir, H, W, k_sigma,
+                                         device, save_video))
+            best, curr = prop.best(), prop.current()
+            stats.update(prop.stats())
+            return _finish(best, best_fit, curr, curr_fit, curves, stats, prefix, loss_png_path,
+                           loss_csv_path, loss_log_y, return_state)
         acc_rate = 0.0                 # EWMA of the per-try acceptance rate
         stats = {"evaluated": 0, "tries": 0, "launches": 0}
         bar = range(iterations)
@@ -145,7 +185,9 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
                         dE = e_new - e_curr                                # annealing.py:133
                         acc = dE <= 0.0
                         if not acc and T > 0.0:
-                            acc = draws.accept() < math.exp(-dE / T)       # annealing.py:140-142
+                            u = draws.accept_at(it, k) if hasattr(draws, "accept_at") else \
+                                draws.accept()
+                            acc = u < math.exp(-dE / T)                    # annealing.py:140-142
                         k += 1
                         acc_rate = 0.9 * acc_rate + 0.1 * float(acc)
                         if acc:
@@ -177,7 +219,64 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
         stats.update(prop.stats())
     finally:
         prop.close()
+    return _finish(best, best_fit, curr, curr_fit, curves, stats, prefix, loss_png_path,
+                   loss_csv_path, loss_log_y, return_state)
 
+
+def device_loop_width(H: int, W: int, tries: int) -> int:
+    """Neighbour capacity of a device-loop round: enough 16x128 strips to fill the
+    GPU's 3,072 raster wave slots several times over (2048^2: 16 neighbours of
+    2,048 strips; 512^2: 64 of 256), never below one iteration's tries."""
+    strips = 4 * (-(-W // 64)) * (-(-H // 128))
+    return max(1, tries, min(64, -(-32768 // strips)))
+
+
+def _device_loop(sa, curves, iterations, tries, sched, temp0, width, chunk, progress, save_video,
+                 frame_every, save_frame):
+    """annealing.py:117-172 on the GPU (ggs_sa_run), ``chunk`` iterations per call."""
+    bar = None
+    if progress:
+        try:
+            from tqdm.auto import tqdm
+            bar = tqdm(total=iterations, desc="SA iterations", leave=True)
+        except ImportError:
+            pass
+    st = sa.loop_state()
+    it = 0
+    try:
+        while it < iterations:
+            n = min(max(1, int(chunk)), iterations - it)
+            if save_video:               # frames fall on chunk ends
+                fe = max(1, frame_every)
+                n = min(n, fe - it % fe)
+            if tries:
+                temps = [_T(sched, temp0, i, iterations) for i in range(it, it + n)]
+                cv = sa.run(it, temps, iterations, tries, width)
+                curves["best"].extend(cv[:, 0].tolist())
+                curves["current"].extend(cv[:, 1].tolist())
+                st = sa.loop_state()
+            else:                        # no tries: the state never moves
+                curves["best"].extend([st["best_fit"]] * n)
+                curves["current"].extend([st["current_fit"]] * n)
+            it += n
+            if save_video and it % max(1, frame_every) == 0:
+                save_frame(it)
+            if bar is not None:
+                bar.update(n)
+                bar.set_postfix(best_mse=f"{st['best_fit']:.6f}", curr_mse=f"{st['current_fit']:.6f}",
+                                T=f"{_T(sched, temp0, it - 1, iterations):.4g}")
+    except KeyboardInterrupt:
+        print("\n[Interrupted] Returning current best…", flush=True)
+    finally:
+        if bar is not None:
+            bar.close()
+    stats = {"evaluated": st["evaluated"], "tries": it * tries, "launches": st["rounds"],
+             "accepted": st["accepted"]}
+    return st["best_fit"], st["current_fit"], stats
+
+
+def _finish(best, best_fit, curr, curr_fit, curves, stats, prefix, loss_png_path, loss_csv_path,
+            loss_log_y, return_state):
     try:                                                                   # annealing.py:174-188
         save_loss_curve_png(curves, loss_png_path, title=f"{prefix} energy (MSE)",
                             xlabel="Iteration", ylabel="MSE", log_y=loss_log_y, dpi=144)

@@ -53,6 +53,21 @@ def _draws_struct(draws, keep, fields=None) -> GaDraws:
     return d
 
 
+class PhiloxAcceptDraws:
+    """The device SA loop's acceptance uniforms (ggs_sa_accept_uniform: Philox keyed
+    by (seed, iteration, try)) for the host loop, so a host-driven run with the
+    device proposer follows the device loop's trajectory exactly."""
+
+    def __init__(self, seed: int):
+        self.seed = int(seed) & (2**64 - 1)
+
+    def accept_at(self, it: int, k: int) -> float:
+        u = C.c_double()
+        check(lib.ggs_sa_accept_uniform(self.seed, int(it), int(k), C.byref(u)),
+              "ggs_sa_accept_uniform")
+        return u.value
+
+
 MUTATION_KEYS = ("u_xy", "u_ab", "u_t", "u_rgb", "u_a", "k_color", "k_xy", "k_ab", "k_t", "n_xy",
                  "n_ab", "n_t", "n_rgba", "swap_i", "swap_pick", "swap_u")
 
@@ -103,6 +118,26 @@ class DeviceSA:
 
     def commit(self, j: int, update_best: bool) -> None:
         check(lib.ggs_sa_commit(self.h, j, int(bool(update_best))), "ggs_sa_commit")
+
+    def run(self, first_it: int, temps, total: int, tries: int, width: int = 0) -> np.ndarray:
+        """Iterations first_it .. first_it+len(temps)-1 of the SA loop on the device
+        (ggs_sa_run): acceptance walk and state updates included, one host sync per
+        batch of rounds.  Returns the [n, 2] (best, current) energy curves."""
+        t = _arr(temps, np.float64)
+        out = np.empty((len(t), 2), np.float64)
+        check(lib.ggs_sa_run(self.h, int(first_it), len(t), int(total), int(tries),
+                             t.ctypes.data_as(_f64p), int(width), out.ctypes.data_as(_f64p)),
+              "ggs_sa_run")
+        return out
+
+    def loop_state(self) -> Dict[str, float]:
+        """Energies and counters of the device loop after the last ``run``."""
+        b, c = C.c_double(), C.c_double()
+        r, e, a = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib.ggs_sa_loop_state(self.h, C.byref(b), C.byref(c), C.byref(r), C.byref(e),
+                                    C.byref(a)), "ggs_sa_loop_state")
+        return {"best_fit": b.value, "current_fit": c.value, "rounds": r.value,
+                "evaluated": e.value, "accepted": a.value}
 
     def read(self):
         cur = np.empty((self.N, 9), np.float32)

@@ -199,6 +199,26 @@ int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_
 int ggs_sa_commit(void* handle, int32_t j, int32_t update_best);
 /* Synchronises; any output may be NULL.  neighbours: [n of the last propose][N][9]. */
 int ggs_sa_read(void* handle, float* current, float* best, float* neighbours);
+/* The SA loop itself on the device (annealing.py:117-155 for iterations
+ * first_it .. first_it+n_its-1): each round mutates the next tries from the
+ * current state (Philox keyed by (seed, it, try), as ggs_sa_propose), evaluates
+ * them in one launch and walks them in order with the Metropolis test of
+ * annealing.py:133-146 — acceptance uniform ggs_sa_accept_uniform(seed, it, try)
+ * — installing the first accepted neighbour (and the best, :148-150) on the GPU;
+ * the host syncs once per batch of rounds, not per try.  temps[i]: temperature of
+ * iteration first_it+i (annealing.py:29-44, the caller's float64); width:
+ * neighbours per round, 0 = adaptive (1 / acceptance rate, at most pop_size);
+ * results do not depend on it.  curves_out[i] = {best, current} energy after
+ * iteration first_it+i (annealing.py:152-155).  A session is driven either by
+ * ggs_sa_run or by ggs_sa_propose/commit, not both. */
+int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iters, int32_t tries,
+               const double* temps, int32_t width, double* curves_out);
+/* The device loop's state after the last ggs_sa_run (any output may be NULL). */
+int ggs_sa_loop_state(void* handle, double* best_fit, double* curr_fit, uint64_t* rounds,
+                      uint64_t* evaluated, uint64_t* accepted);
+/* The acceptance uniform in [0, 1) ggs_sa_run draws for try k of iteration it
+ * (lets a host loop reproduce the device loop's trajectory). */
+int ggs_sa_accept_uniform(uint64_t seed, int32_t it, int32_t k, double* u);
 /* Incremental evaluation (default off): a neighbour's 16-column strips that no
  * changed splat touches (old or new AABB) keep the current state's partial sums —
  * bit-identical to a full re-render; off = every strip is rasterised. */

@@ -225,3 +225,66 @@ def test_device_sa_incremental_equals_full_rerender(H, W, N, mutpb, boost):
     assert f1 == f0 and s1["curves"] == s0["curves"]
     assert s1["stats"]["proposed"] == s1["stats"]["evaluated"] > 0
     assert 0 < s1["stats"]["changed_splats"] <= s1["stats"]["proposed"] * N
+
+
+@pytest.mark.parametrize("H,W,N,tries,spec,inc,iters", [(40, 40, 17, 4, None, False, 9),
+                                                        (64, 48, 300, 3, 5, False, 7),
+                                                        (48, 48, 2, 8, 1, False, 6),
+                                                        (96, 80, 64, 6, None, True, 8),
+                                                        # unfused prep (N > 1024), SAT raster
+                                                        (64, 64, 1100, 3, 2, False, 4)])
+def test_device_loop_matches_host_loop(H, W, N, tries, spec, inc, iters):
+    """ggs_sa_run (iterations, Metropolis test and installs on the GPU) follows
+    the host-driven loop over the same device proposer and the same Philox
+    acceptance uniforms try for try: same states, energies and curves.  High T0
+    so that acceptances (and re-proposed rounds) are frequent."""
+    target, _, _ = _problem(H, W, 7)
+    init = ga.new_population(1, N, H, W, MIN_S, MAX_S, np.random.default_rng(N + 1))[0]
+    kw = dict(tries_per_iter=tries, speculate=spec, init_individual=init, iterations=iters,
+              temp0=5e-2, backend="device", seed=11, incremental=inc)
+    hb, hf, hs = _sa(target, H, W, N, loop="host", **kw)
+    for chunk in (3, 256):
+        db, df, ds = _sa(target, H, W, N, loop="device", chunk=chunk, **kw)
+        np.testing.assert_array_equal(db, hb)
+        np.testing.assert_array_equal(ds["current"], hs["current"])
+        assert df == hf and ds["curves"] == hs["curves"]
+        assert ds["current_fit"] == hs["current_fit"]
+        assert ds["stats"]["tries"] == hs["stats"]["tries"] == iters * tries
+        assert 0 < ds["stats"]["accepted"] and ds["stats"]["evaluated"] >= iters * tries
+
+
+def test_device_loop_width_invariant_low_temperature():
+    """Rare acceptances: rounds span several iterations (width up to the cap);
+    the trajectory does not depend on the width or the chunking."""
+    H = W = 128
+    target, t, m = _problem(H, W, 8)
+    init = ga.new_population(1, 96, H, W, MIN_S, MAX_S, np.random.default_rng(2))[0]
+    kw = dict(tries_per_iter=5, iterations=40, temp0=1e-6, backend="device", seed=5,
+              init_individual=init)
+    outs = [_sa(target, H, W, 96, speculate=s, chunk=c, **kw)
+            for s, c in ((None, 256), (1, 7), (13, 256), (None, 1))]
+    for b, f, st in outs[1:]:
+        np.testing.assert_array_equal(b, outs[0][0])
+        assert f == outs[0][1] and st["curves"] == outs[0][2]["curves"]
+    assert outs[0][2]["stats"]["launches"] < 40      # rounds held more than one iteration
+    assert outs[1][2]["stats"]["evaluated"] == outs[1][2]["stats"]["launches"]   # width 1
+    b, f, _ = outs[0]
+    assert float(ggs.fitness(b[None], t, H, W, 3.0, weight_mask=m)[0]) == f
+
+
+def test_device_loop_rejects_mixed_driving():
+    from ggs.ga_device import DeviceSA
+    H = W = 32
+    _, t, m = _problem(H, W, 1)
+    init = ga.new_population(1, 8, H, W, MIN_S, MAX_S, np.random.default_rng(0))[0]
+    sa = DeviceSA(t, m, init, max_tries=4, mutpb=0.1, schedule="cosine", min_scale_splats=MIN_S,
+                  max_scale_splats=MAX_S, mut_sigma_max=CFG["mut_sigma_max"],
+                  mut_sigma_min=CFG["mut_sigma_min"], seed=1)
+    try:
+        with pytest.raises(AssertionError):           # GGS_EINVAL
+            sa.run(0, [1e-3], 1, 2, width=5)          # width above the capacity
+        sa.run(0, [1e-3, 1e-3], 2, 2)
+        with pytest.raises(AssertionError):
+            sa.propose(0, 2, 0, 2)
+    finally:
+        sa.close()

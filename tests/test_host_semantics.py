@@ -141,3 +141,29 @@ def test_file_rendezvous_carries_rank0s_id_to_every_rank(tmp_path):
 def test_file_rendezvous_times_out_without_rank0(tmp_path):
     with pytest.raises(TimeoutError):
         file_rendezvous(1, 2, lambda: b"", key="nobody", directory=str(tmp_path), timeout_s=0.2)
+
+
+def _philox_u53(seed: int, it: int, k: int) -> float:
+    """Philox4x32-10 (Salmon et al., SC'11) on counter (it, k, 0, 8), key = seed,
+    restated in Python integers: the acceptance uniform the device SA loop draws."""
+    M = 0xFFFFFFFF
+    c = [it & M, k & M, 0, 8]
+    k0, k1 = seed & M, (seed >> 32) & M
+    for _ in range(10):
+        p0, p1 = 0xD2511F53 * c[0], 0xCD9E8D57 * c[2]
+        c = [((p1 >> 32) ^ c[1] ^ k0) & M, p1 & M, ((p0 >> 32) ^ c[3] ^ k1) & M, p0 & M]
+        k0, k1 = (k0 + 0x9E3779B9) & M, (k1 + 0xBB67AE85) & M
+    return ((c[0] >> 5) * 67108864.0 + (c[1] >> 6)) / 9007199254740992.0
+
+
+def test_sa_accept_uniform_is_philox():
+    """ggs_sa_accept_uniform (host code in libggs, the same function the device
+    loop's accept kernel calls) against an independent restatement."""
+    from ggs.ga_device import PhiloxAcceptDraws
+    for seed in (0, 42, 2**63 + 12345):
+        d = PhiloxAcceptDraws(seed)
+        us = [d.accept_at(it, k) for it in (0, 1, 7, 1000) for k in range(5)]
+        assert us == [_philox_u53(seed, it, k) for it in (0, 1, 7, 1000) for k in range(5)]
+        assert all(0.0 <= u < 1.0 for u in us) and len(set(us)) == len(us)
+    with pytest.raises(Exception):
+        PhiloxAcceptDraws(0).accept_at(-1, 0)

@@ -5,11 +5,15 @@ importance mask, initial evaluation — is timed separately and subtracted):
 * host / sequential: numpy mutation, one host-API launch per try (the
   reference's schedule);
 * host / speculative: numpy mutation, batched tries;
-* device / speculative: state resident in HBM, in-kernel mutation (Philox),
-  batched tries, one 4-byte-per-try readback per batch; "full" re-rasterises
-  every strip, "incremental" only the strips a changed splat touches.
+* device / host loop: state resident in HBM, in-kernel mutation (Philox),
+  batched tries, one 4-byte-per-try readback and host acceptance test per batch;
+* device / device loop (ggs_sa_run, the default): acceptance walk and state
+  installs on the GPU too, rounds spanning iterations, one host sync per batch
+  of rounds; "full" re-rasterises every strip, "incremental" only the strips a
+  changed splat touches.  Timed --repeat times over --dev-iters iterations.
 
-usage: python tools/bench_sa.py [--iters 20] [--size 2048] [--splats 4096] [--tries 8]"""
+usage: python tools/bench_sa.py [--iters 20] [--dev-iters 200] [--repeat 3] [--size 2048]
+                                [--splats 4096] [--tries 8] [--only device_loop_full]"""
 import argparse, json, os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -23,6 +27,10 @@ ap.add_argument("--size", type=int, default=2048)
 ap.add_argument("--splats", type=int, default=4096)
 ap.add_argument("--tries", type=int, default=8)
 ap.add_argument("--mutpb", type=float, default=0.05)
+ap.add_argument("--dev-iters", type=int, default=200)
+ap.add_argument("--repeat", type=int, default=3)
+ap.add_argument("--temp0", type=float, default=1e-3)
+ap.add_argument("--only", default="")
 a = ap.parse_args()
 H = W = a.size
 target = np.random.default_rng(0).uniform(0, 1, (H, W, 3)).astype(np.float32)
@@ -44,32 +52,49 @@ def evaluate(G):
 
 
 res = {}
-for name, spec, backend, inc in (("host_sequential", 1, "host", False),
-                                 ("host_speculative", None, "host", False),
-                                 ("device_speculative_full", None, "device", False),
-                                 ("device_speculative_incremental", None, "device", True)):
+variants = (("host_sequential", 1, "host", False, "host"),
+            ("host_speculative", None, "host", False, "host"),
+            ("device_host_loop", None, "device", False, "host"),
+            ("device_loop_full", None, "device", False, "device"),
+            ("device_loop_incremental", None, "device", True, "device"))
+for name, spec, backend, inc, loop in variants:
+    if a.only and name not in a.only.split(","):
+        continue
     run = lambda n: A.simulated_annealing(          # noqa: E731
         target, H, W, "cuda", a.splats, a.mutpb, cfg["mut_sigma_max"], cfg["mut_sigma_min"],
-        "cosine", 3.0, 0.1, 3.0, 0.7, False, n, 1e-3, "cosine", a.tries, seed=2,
+        "cosine", 3.0, 0.1, 3.0, 0.7, False, n, a.temp0, "cosine", a.tries, seed=2,
         init_individual=init, evaluate=evaluate if backend == "host" else None, progress=False,
-        return_state=True, speculate=spec, backend=backend, incremental=inc)
+        return_state=True, speculate=spec, backend=backend, incremental=inc, loop=loop)
+    iters = a.dev_iters if loop == "device" else a.iters
+    reps = a.repeat if loop == "device" else 1
     run(2)                                           # warm-up
     t0 = time.perf_counter()
     run(0)                                           # setup only
     t_setup = time.perf_counter() - t0
-    ev["s"] = 0.0
-    t0 = time.perf_counter()
-    best, fit, st = run(a.iters)
-    dt = time.perf_counter() - t0 - t_setup
-    res[name] = {"iters_per_s": round(a.iters / dt, 2), "ms_per_iter": round(dt / a.iters * 1e3, 2),
-                 "setup_ms": round(t_setup * 1e3, 1),
+    rates = []
+    for _ in range(reps):
+        ev["s"] = 0.0
+        t0 = time.perf_counter()
+        best, fit, st = run(iters)
+        dt = time.perf_counter() - t0 - t_setup
+        rates.append(iters / dt)
+    dt = iters / sorted(rates)[len(rates) // 2]
+    res[name] = {"iters_per_s": round(iters / dt, 2), "ms_per_iter": round(dt / iters * 1e3, 2),
+                 "iters": iters, "runs_iters_per_s": [round(r, 1) for r in rates],
+                 "setup_ms": round(t_setup * 1e3, 1), "accepted": st["stats"].get("accepted"),
                  "eval_ms_per_iter": round(ev["s"] / a.iters * 1e3, 2) if backend == "host" else None,
                  "launches": st["stats"]["launches"], "evaluated": st["stats"]["evaluated"],
                  "changed_splats_per_neighbour": round(st["stats"]["changed_splats"] /
                                                        max(1, st["stats"]["proposed"]), 1)
                  if "changed_splats" in st["stats"] else None,
                  "best_fit": fit}
-assert res["host_sequential"]["best_fit"] == res["host_speculative"]["best_fit"]
-assert res["device_speculative_full"]["best_fit"] == res["device_speculative_incremental"]["best_fit"]
+def same(x, y):
+    if x in res and y in res and res[x]["iters"] == res[y]["iters"]:
+        assert res[x]["best_fit"] == res[y]["best_fit"], (x, y)
+
+
+same("host_sequential", "host_speculative")
+same("device_host_loop", "device_loop_full")
+same("device_loop_full", "device_loop_incremental")
 print(json.dumps({"metric": "SA iterations/s", "config": {"H": H, "W": W, "splats": a.splats,
                   "tries_per_iter": a.tries, "mutpb": a.mutpb, "iters": a.iters}, **res}))
