@@ -1029,6 +1029,7 @@ struct SaSession {
     DevBuf curr, best, nb, nb_fits, target, mask, draws;
     DevBuf cur_recs, nb_recs, cur_part, nb_part, dirty, plan, wpart, order, counters;
     DevBuf loop, sit, curves;       // device SA loop (ggs_sa_run): state, per-iteration table, curves
+    DevBuf flags, sizes;            // ... and its mutation scratch (per-try mask-group flags, splat sizes)
     float* h_fits = nullptr;        // pinned
     unsigned* h_counters = nullptr; // pinned: [0] changed splats (last propose)
     SaLoopDev* h_loop = nullptr;    // pinned copy of the loop state
@@ -1039,7 +1040,7 @@ struct SaSession {
 void sa_free(SaSession* s) {
     for (DevBuf* b : {&s->curr, &s->best, &s->nb, &s->nb_fits, &s->target, &s->mask, &s->draws,
                       &s->cur_recs, &s->nb_recs, &s->cur_part, &s->nb_part, &s->dirty, &s->plan,
-                      &s->wpart, &s->order, &s->counters, &s->loop, &s->sit, &s->curves})
+                      &s->wpart, &s->order, &s->counters, &s->loop, &s->sit, &s->curves, &s->flags, &s->sizes})
         if (b->p) (void)hipFree(b->p);
     if (s->h_loop) (void)hipHostFree(s->h_loop);
     if (s->h_fits) (void)hipHostFree(s->h_fits);
@@ -1299,7 +1300,8 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
         (rc = ensure(s->dirty, slots * s->cap, s->st)) || (rc = ensure(s->plan, plan_bytes(cfg->H, cfg->W), s->st)) ||
         (rc = ensure(s->wpart, sizeof(float) * slots, s->st)) ||
         (rc = ensure(s->order, sizeof(int) * (size_t)raster_order_len(cfg->H, cfg->W), s->st)) ||
-        (rc = ensure(s->counters, sizeof(unsigned) * 4, s->st)) || (rc = ensure(s->loop, sizeof(SaLoopDev), s->st)))
+        (rc = ensure(s->counters, sizeof(unsigned) * 4, s->st)) || (rc = ensure(s->loop, sizeof(SaLoopDev), s->st)) ||
+        (rc = ensure(s->sizes, sizeof(float) * (size_t)std::max(s->N, 1) * s->cap, s->st)))
         return bail(rc);
     if (hipHostMalloc((void**)&s->h_fits, sizeof(float) * s->cap, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&s->h_counters, sizeof(unsigned) * 4, hipHostMallocDefault) != hipSuccess ||
@@ -1428,23 +1430,39 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
     GGS_HIP(hipMemcpyAsync(s->sit.p, tab.data(), sizeof(SaItDev) * (size_t)n_its, hipMemcpyHostToDevice, s->st));
     const int64_t pos0 = (int64_t)first_it * tries, end = pos0 + (int64_t)n_its * tries;
     GGS_HIP(launch_sa_begin(s->st, loop, pos0, end, tries, first_it, s->cap, width));
+    if ((rc = ensure(s->flags, sizeof(int) * (size_t)(end - pos0), s->st))) return rc;
+    GGS_HIP(launch_sa_flags(s->st, pos0, (int)(end - pos0), tries, c.seed, c.mutpb, s->N, (int*)s->flags.p));
     GaParamsDev prm = ga_params(c, first_it, total_iters);   // sigmas replaced per neighbour from sit
     prm.mutate_only = 1;
     prm.o_base = 0;
-    const bool fuse_prep = s->N <= 1024 || s->cap >= 64;     // as ggs_sa_propose
     const int nslots = 4 * s->nTiles;
     const float bg[3] = {1.f, 1.f, 1.f};
     const int* live = &loop->live;
+    SaRoundDev rd{};
+    rd.partials = (const float*)s->nb_part.p;
+    rd.wpartials = (const float*)s->wpart.p;
+    rd.nslots = nslots;
+    rd.mode = c.fitness_mode;
+    rd.N = s->N;
+    rd.hw = (double)c.H * (double)c.W;
+    rd.fits_out = (float*)s->nb_fits.p;
+    rd.seed = c.seed;
+    rd.mutpb = c.mutpb;
+    rd.curves = curves;
+    rd.curr = (float*)s->curr.p;
+    rd.best = (float*)s->best.p;
+    rd.nb = (const float*)s->nb.p;
+    rd.cur_recs = s->incremental ? (SplatRec*)s->cur_recs.p : nullptr;
+    rd.nb_recs = (const SplatRec*)s->nb_recs.p;
+    rd.cur_part = (float*)s->cur_part.p;
+    // one round: mutate (+ records) and swap, [dirty strips], raster, then one
+    // workgroup for fitness, acceptance, install and the next round's flags
     auto round = [&]() -> int {
         {
             ProfScope ps(s->st, 0);
-            GGS_HIP(launch_ga_variation(s->st, (const float*)s->curr.p, nullptr, 1, s->N, prm, GaDrawsDev{}, c.seed,
-                                        first_it, (float*)s->nb.p, s->cap,
-                                        fuse_prep ? (SplatRec*)s->nb_recs.p : nullptr, c.H, c.W, c.k_sigma, loop,
-                                        sit));
-            if (!fuse_prep)
-                GGS_HIP(launch_prep(s->st, true, (const float*)s->nb.p, (int64_t)s->cap * s->N, 9, c.H, c.W,
-                                    c.k_sigma, (SplatRec*)s->nb_recs.p, nullptr, nullptr, nullptr, live, s->N));
+            GGS_HIP(launch_sa_mutate(s->st, loop, sit, prm, c.seed, s->N, s->cap, (int*)s->flags.p,
+                                     (const float*)s->curr.p, (float*)s->nb.p, (float*)s->sizes.p,
+                                     (SplatRec*)s->nb_recs.p, c.H, c.W, c.k_sigma));
         }
         if (s->incremental)
             GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, (const float*)s->nb.p,
@@ -1457,16 +1475,7 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
                                   s->incremental ? (const unsigned char*)s->dirty.p : nullptr,
                                   (const float*)s->cur_part.p, live));
         }
-        {
-            ProfScope ps(s->st, 2);
-            GGS_HIP(launch_finalize(s->st, (const float*)s->nb_part.p, (const float*)s->wpart.p, s->cap, s->nTiles,
-                                    c.fitness_mode, c.H, c.W, (float*)s->nb_fits.p, live));
-        }
-        GGS_HIP(launch_sa_accept(s->st, loop, sit, (const float*)s->nb_fits.p, c.seed, curves, (float*)s->curr.p,
-                                 (float*)s->best.p, (const float*)s->nb.p, s->N,
-                                 s->incremental ? (SplatRec*)s->cur_recs.p : nullptr,
-                                 (const SplatRec*)s->nb_recs.p, (float*)s->cur_part.p,
-                                 (const float*)s->nb_part.p, nslots));
+        GGS_HIP(launch_sa_accept(s->st, loop, sit, rd));
         return GGS_OK;
     };
     // Rounds are enqueued in batches with one host sync between batches: a round

@@ -101,6 +101,95 @@ __device__ int tournament_pick(const float* __restrict__ fits, const GaDrawsDev&
     return best;
 }
 
+// Per-splat pieces of the variation, shared by the GA variation kernel and the
+// SA loop's split kernels (same code, so the same bits).
+struct MaskU {                  // mask uniforms of one splat (genetic.py:37-54)
+    float ux0, ux1, ua0, ua1, ut, urgb, ua;
+};
+__device__ __forceinline__ MaskU mask_draws(const GaDrawsDev& d, const Rng& rng, uint32_t og, int64_t ob, int s) {
+    MaskU m;
+    if (d.u_xy) {
+        m.ux0 = d.u_xy[(ob + s) * 2]; m.ux1 = d.u_xy[(ob + s) * 2 + 1];
+        m.ua0 = d.u_ab[(ob + s) * 2]; m.ua1 = d.u_ab[(ob + s) * 2 + 1];
+        m.ut = d.u_t[ob + s]; m.urgb = d.u_rgb[ob + s]; m.ua = d.u_a[ob + s];
+    } else {
+        const U4 r1 = rng.block(S_MASK, og, (uint32_t)(2 * s));
+        const U4 r2 = rng.block(S_MASK, og, (uint32_t)(2 * s + 1));
+        m.ux0 = u01(r1.x); m.ux1 = u01(r1.y); m.ua0 = u01(r1.z); m.ua1 = u01(r1.w);
+        m.ut = u01(r2.x); m.urgb = u01(r2.y); m.ua = u01(r2.z);
+    }
+    return m;
+}
+enum : int { ANY_COLOR = 1, ANY_XY = 2, ANY_AB = 4, ANY_T = 8 };
+__device__ __forceinline__ int mask_any(const MaskU& m, float p) {
+    return (((m.urgb < p) | (m.ua < p)) ? ANY_COLOR : 0) | (((m.ux0 < p) | (m.ux1 < p)) ? ANY_XY : 0) |
+           (((m.ua0 < p) | (m.ua1 < p)) ? ANY_AB : 0) | ((m.ut < p) ? ANY_T : 0);
+}
+struct Fallback {               // genetic.py:24-29: one-true flat indices (-1: not needed)
+    int kc, kx, kb, kt;
+};
+__device__ __forceinline__ Fallback fallbacks(const GaDrawsDev& d, const Rng& rng, uint32_t og, int o, int N,
+                                              int any) {
+    Fallback f{-1, -1, -1, -1};
+    if (!(any & ANY_COLOR)) f.kc = d.k_color ? d.k_color[o] : (int)(rng.block(S_IND, og, 0).x % (uint32_t)(2 * N));
+    if (!(any & ANY_XY)) f.kx = d.k_xy ? d.k_xy[o] : (int)(rng.block(S_IND, og, 1).x % (uint32_t)(2 * N));
+    if (!(any & ANY_AB)) f.kb = d.k_ab ? d.k_ab[o] : (int)(rng.block(S_IND, og, 2).x % (uint32_t)(2 * N));
+    if (!(any & ANY_T)) f.kt = d.k_t ? d.k_t[o] : (int)(rng.block(S_IND, og, 3).x % (uint32_t)N);
+    return f;
+}
+struct NormD {                  // normals of one splat (genetic.py:57-70)
+    float nx0, nx1, na0, na1, nt, nr0, nr1, nr2, nr3;
+};
+__device__ __forceinline__ NormD normal_draws(const GaDrawsDev& d, const Rng& rng, uint32_t og, int64_t ob, int s,
+                                              int N) {
+    NormD n;
+    if (d.u_xy) {
+        n.nx0 = d.n_xy[(ob + s) * 2]; n.nx1 = d.n_xy[(ob + s) * 2 + 1];
+        n.na0 = d.n_ab[(ob + s) * 2]; n.na1 = d.n_ab[(ob + s) * 2 + 1];
+        n.nt = d.n_t[ob + s];
+        n.nr0 = d.n_rgba[(ob + s) * 4]; n.nr1 = d.n_rgba[(ob + s) * 4 + 1];
+        n.nr2 = d.n_rgba[(ob + s) * 4 + 2]; n.nr3 = d.n_rgba[(ob + s) * 4 + 3];
+    } else {
+        const U4 g1 = rng.block(S_NORM_A, og, (uint32_t)s);
+        const U4 g2 = rng.block(S_NORM_B, og, (uint32_t)s);
+        const U4 g3 = rng.block(S_NORM_C, og, (uint32_t)s);
+        n.nx0 = normal_from(g1.x, g1.y); n.nx1 = normal_from(g1.z, g1.w);
+        n.na0 = normal_from(g2.x, g2.y); n.na1 = normal_from(g2.z, g2.w);
+        n.nt = normal_from(g3.x, g3.y); n.nr0 = normal_from(g3.z, g3.w);
+        const U4 g4 = rng.block(S_NORM_C, og, (uint32_t)(s + N));
+        n.nr1 = normal_from(g4.x, g4.y); n.nr2 = normal_from(g4.z, g4.w);
+        const U4 g5 = rng.block(S_NORM_C, og, (uint32_t)(s + 2 * N));
+        n.nr3 = normal_from(g5.x, g5.y);
+    }
+    return n;
+}
+// genetic.py:37-70 + clamp_genome (utils.py:35-45) on one row, ggs/ga.py's float32 op order
+__device__ __forceinline__ void mutate_row(float* g, const MaskU& u, const NormD& n, const Fallback& f, int s,
+                                           const GaParamsDev& prm) {
+    const float p = prm.mutpb;
+    const bool mrgb = (u.urgb < p) || (f.kc == 2 * s), ma = (u.ua < p) || (f.kc == 2 * s + 1);
+    const bool mx0 = (u.ux0 < p) || (f.kx == 2 * s), mx1 = (u.ux1 < p) || (f.kx == 2 * s + 1);
+    const bool mb0 = (u.ua0 < p) || (f.kb == 2 * s), mb1 = (u.ua1 < p) || (f.kb == 2 * s + 1);
+    const bool mt = (u.ut < p) || (f.kt == s);
+    g[0] = g[0] + (n.nx0 * prm.sig_xy) * (float)mx0;
+    g[1] = g[1] + (n.nx1 * prm.sig_xy) * (float)mx1;
+    g[2] = g[2] + (n.na0 * prm.sig_alog) * (float)mb0;
+    g[3] = g[3] + (n.na1 * prm.sig_blog) * (float)mb1;
+    g[4] = g[4] + (n.nt * prm.sig_theta) * (float)mt;
+    g[4] = wrap_angle(g[4]);
+    g[5] = g[5] + (n.nr0 * prm.sig_rgb) * (float)mrgb;
+    g[6] = g[6] + (n.nr1 * prm.sig_rgb) * (float)mrgb;
+    g[7] = g[7] + (n.nr2 * prm.sig_rgb) * (float)mrgb;
+    g[8] = g[8] + (n.nr3 * prm.sig_alpha) * (float)ma;
+    g[0] = clip(g[0], 0.0f, 1.0f);
+    g[1] = clip(g[1], 0.0f, 1.0f);
+    g[2] = clip(g[2], prm.log_lo, prm.log_hi);
+    g[3] = clip(g[3], prm.log_lo, prm.log_hi);
+    g[4] = wrap_angle(g[4]);
+#pragma unroll
+    for (int c = 5; c < 9; ++c) g[c] = clip(g[c], 0.0f, 255.0f);
+}
+
 // Threads per variation workgroup (one workgroup per offspring): 256 for a GA
 // generation (P workgroups fill the chip); 1024 when a few large offspring are
 // bred (SA tries at configs[4]: 4,096 splats each), which otherwise leave 16
@@ -154,66 +243,20 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
     const int64_t ob = (int64_t)o * N;
 
     // pass 1: crossover + mask flags, any() per mask group
-    int any_color = 0, any_xy = 0, any_ab = 0, any_t = 0;
-    for (int s = tid; s < N; s += VT) {
-        float ux0, ux1, ua0, ua1, ut, urgb, ua;
-        if (d.u_xy) {
-            ux0 = d.u_xy[(ob + s) * 2]; ux1 = d.u_xy[(ob + s) * 2 + 1];
-            ua0 = d.u_ab[(ob + s) * 2]; ua1 = d.u_ab[(ob + s) * 2 + 1];
-            ut = d.u_t[ob + s]; urgb = d.u_rgb[ob + s]; ua = d.u_a[ob + s];
-        } else {
-            const U4 r1 = rng.block(S_MASK, og, (uint32_t)(2 * s));
-            const U4 r2 = rng.block(S_MASK, og, (uint32_t)(2 * s + 1));
-            ux0 = u01(r1.x); ux1 = u01(r1.y); ua0 = u01(r1.z); ua1 = u01(r1.w);
-            ut = u01(r2.x); urgb = u01(r2.y); ua = u01(r2.z);
-        }
-        any_color |= (urgb < p) | (ua < p);
-        any_xy |= (ux0 < p) | (ux1 < p);
-        any_ab |= (ua0 < p) | (ua1 < p);
-        any_t |= (ut < p);
-    }
-    any_color = __syncthreads_or(any_color);
-    any_xy = __syncthreads_or(any_xy);
-    any_ab = __syncthreads_or(any_ab);
-    any_t = __syncthreads_or(any_t);
+    int any = 0;
+    for (int s = tid; s < N; s += VT) any |= mask_any(mask_draws(d, rng, og, ob, s), p);
+    any = (__syncthreads_or(any & ANY_COLOR) ? ANY_COLOR : 0) | (__syncthreads_or(any & ANY_XY) ? ANY_XY : 0) |
+          (__syncthreads_or(any & ANY_AB) ? ANY_AB : 0) | (__syncthreads_or(any & ANY_T) ? ANY_T : 0);
     // genetic.py:24-29: fallback flat indices (k into [N,2] or [N,1] row-major)
-    int kc = -1, kx = -1, kb = -1, kt = -1;
-    if (!any_color) kc = d.k_color ? d.k_color[o] : (int)(rng.block(S_IND, og, 0).x % (uint32_t)(2 * N));
-    if (!any_xy) kx = d.k_xy ? d.k_xy[o] : (int)(rng.block(S_IND, og, 1).x % (uint32_t)(2 * N));
-    if (!any_ab) kb = d.k_ab ? d.k_ab[o] : (int)(rng.block(S_IND, og, 2).x % (uint32_t)(2 * N));
-    if (!any_t) kt = d.k_t ? d.k_t[o] : (int)(rng.block(S_IND, og, 3).x % (uint32_t)N);
+    const Fallback fb = fallbacks(d, rng, og, o, N, any);
 
     // pass 2: build the child row, mutate, wrap, clamp -> off
     for (int s = tid; s < N; s += VT) {
-        float ux0, ux1, ua0, ua1, ut, urgb, ua, cxu = 0.0f;
-        float nx0, nx1, na0, na1, nt, nr0, nr1, nr2, nr3;
-        if (d.u_xy) {
-            ux0 = d.u_xy[(ob + s) * 2]; ux1 = d.u_xy[(ob + s) * 2 + 1];
-            ua0 = d.u_ab[(ob + s) * 2]; ua1 = d.u_ab[(ob + s) * 2 + 1];
-            ut = d.u_t[ob + s]; urgb = d.u_rgb[ob + s]; ua = d.u_a[ob + s];
-            nx0 = d.n_xy[(ob + s) * 2]; nx1 = d.n_xy[(ob + s) * 2 + 1];
-            na0 = d.n_ab[(ob + s) * 2]; na1 = d.n_ab[(ob + s) * 2 + 1];
-            nt = d.n_t[ob + s];
-            nr0 = d.n_rgba[(ob + s) * 4]; nr1 = d.n_rgba[(ob + s) * 4 + 1];
-            nr2 = d.n_rgba[(ob + s) * 4 + 2]; nr3 = d.n_rgba[(ob + s) * 4 + 3];
-            if (s_cx) cxu = d.cx_u[(int64_t)pair * N + s];
-        } else {
-            const U4 r1 = rng.block(S_MASK, og, (uint32_t)(2 * s));
-            const U4 r2 = rng.block(S_MASK, og, (uint32_t)(2 * s + 1));
-            ux0 = u01(r1.x); ux1 = u01(r1.y); ua0 = u01(r1.z); ua1 = u01(r1.w);
-            ut = u01(r2.x); urgb = u01(r2.y); ua = u01(r2.z);
-            const U4 g1 = rng.block(S_NORM_A, og, (uint32_t)s);
-            const U4 g2 = rng.block(S_NORM_B, og, (uint32_t)s);
-            const U4 g3 = rng.block(S_NORM_C, og, (uint32_t)s);
-            nx0 = normal_from(g1.x, g1.y); nx1 = normal_from(g1.z, g1.w);
-            na0 = normal_from(g2.x, g2.y); na1 = normal_from(g2.z, g2.w);
-            nt = normal_from(g3.x, g3.y); nr0 = normal_from(g3.z, g3.w);
-            const U4 g4 = rng.block(S_NORM_C, og, (uint32_t)(s + N));
-            nr1 = normal_from(g4.x, g4.y); nr2 = normal_from(g4.z, g4.w);
-            const U4 g5 = rng.block(S_NORM_C, og, (uint32_t)(s + 2 * N));
-            nr3 = normal_from(g5.x, g5.y);
-            if (s_cx) cxu = u01(rng.block(S_CX, (uint32_t)pair, (uint32_t)(s + 1)).x);   // shared by the pair
-        }
+        const MaskU u = mask_draws(d, rng, og, ob, s);
+        const NormD nd = normal_draws(d, rng, og, ob, s, N);
+        float cxu = 0.0f;
+        if (s_cx) cxu = d.cx_u ? d.cx_u[(int64_t)pair * N + s]
+                               : u01(rng.block(S_CX, (uint32_t)pair, (uint32_t)(s + 1)).x);   // shared by the pair
         // genetic.py:17-21 (c1 = where(m, a, b), c2 = where(m, b, a)) / duplicate
         const bool m = cxu < 0.5f;
         const bool takeA = s_cx ? (first ? m : !m) : first;
@@ -221,30 +264,7 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
         float g[9];
 #pragma unroll
         for (int c = 0; c < 9; ++c) g[c] = src[c];
-        // flags (genetic.py:37-54) with the one-true fallbacks
-        const bool mrgb = (urgb < p) || (kc == 2 * s), ma = (ua < p) || (kc == 2 * s + 1);
-        const bool mx0 = (ux0 < p) || (kx == 2 * s), mx1 = (ux1 < p) || (kx == 2 * s + 1);
-        const bool mb0 = (ua0 < p) || (kb == 2 * s), mb1 = (ua1 < p) || (kb == 2 * s + 1);
-        const bool mt = (ut < p) || (kt == s);
-        // genetic.py:57-70, same float32 op order as ggs/ga.py
-        g[0] = g[0] + (nx0 * prm.sig_xy) * (float)mx0;
-        g[1] = g[1] + (nx1 * prm.sig_xy) * (float)mx1;
-        g[2] = g[2] + (na0 * prm.sig_alog) * (float)mb0;
-        g[3] = g[3] + (na1 * prm.sig_blog) * (float)mb1;
-        g[4] = g[4] + (nt * prm.sig_theta) * (float)mt;
-        g[4] = wrap_angle(g[4]);
-        g[5] = g[5] + (nr0 * prm.sig_rgb) * (float)mrgb;
-        g[6] = g[6] + (nr1 * prm.sig_rgb) * (float)mrgb;
-        g[7] = g[7] + (nr2 * prm.sig_rgb) * (float)mrgb;
-        g[8] = g[8] + (nr3 * prm.sig_alpha) * (float)ma;
-        // clamp_genome (utils.py:35-45)
-        g[0] = clip(g[0], 0.0f, 1.0f);
-        g[1] = clip(g[1], 0.0f, 1.0f);
-        g[2] = clip(g[2], prm.log_lo, prm.log_hi);
-        g[3] = clip(g[3], prm.log_lo, prm.log_hi);
-        g[4] = wrap_angle(g[4]);
-#pragma unroll
-        for (int c = 5; c < 9; ++c) g[c] = clip(g[c], 0.0f, 255.0f);
+        mutate_row(g, u, nd, fb, s, prm);      // flags with the one-true fallbacks, mutation, clamp
 #pragma unroll
         for (int c = 0; c < 9; ++c) O[(int64_t)s * 9 + c] = g[c];
     }
@@ -544,33 +564,198 @@ __device__ __forceinline__ int sa_width(const SaLoopDev& s) {
     return (int)min((int64_t)w, max(s.end - s.pos, (int64_t)0));
 }
 
-__global__ void sa_begin_kernel(SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it, int cap,
-                                int width) {
-    sl->pos = pos;
-    sl->end = end;
-    sl->tries = tries;
-    sl->first_it = first_it;
-    sl->cap = cap;
-    sl->width = width;
-    sl->acc_j = -1;
-    sl->new_best = 0;
-    sl->live = sa_width(*sl);
+// The round's neighbours, spread over the GPU: ga_variation_kernel gives each
+// neighbour one workgroup, so a round of a few 4,096-splat neighbours ran on a
+// few CUs (40 us + a 5-us prep launch).  Here three kernels of one workgroup per
+// (neighbour, 256 splats) — flags, mutate + prep, swap — do the same per-splat
+// work with the same helpers (the same bits as ggs_sa_propose's variation).
+constexpr int SA_VT = 256;
+
+struct SaTry {                  // neighbour o of the round -> its Philox identity and sigmas
+    uint32_t og;
+    int gen;
+};
+__device__ __forceinline__ SaTry sa_try(const SaLoopDev& s, const SaItDev* sit, int o, GaParamsDev& prm) {
+    const int64_t g = s.pos + o;
+    const int it = (int)(g / s.tries);
+    const SaItDev& q = sit[it - s.first_it];
+    prm.sig_xy = q.sig[0]; prm.sig_alog = q.sig[1]; prm.sig_blog = q.sig[2];
+    prm.sig_theta = q.sig[3]; prm.sig_rgb = q.sig[4]; prm.sig_alpha = q.sig[5];
+    return {(uint32_t)(g % s.tries), it};
 }
 
-// annealing.py:130-150 over the round's neighbours, in try order, by one thread;
-// then the workgroup installs the accepted neighbour.  Same arithmetic as the
+// pass 1, for every try of the chunk at once (the mask uniforms do not depend on
+// the state, so a try re-proposed after an acceptance keeps its flags): any() of
+// each mask group over try t's splats -> tflags[t] (OR; zeroed by the caller)
+__global__ void __launch_bounds__(SA_VT)
+sa_flags_kernel(int64_t pos0, int tries, uint32_t k0, uint32_t k1, float mutpb, int N, int nch,
+                int* __restrict__ tflags) {
+    const int t = blockIdx.x / nch, s = (blockIdx.x % nch) * SA_VT + threadIdx.x;
+    const int64_t g = pos0 + t;
+    const Rng rng{k0, k1, (uint32_t)(g / tries)};
+    const int any = s < N ? mask_any(mask_draws(GaDrawsDev{}, rng, (uint32_t)(g % tries), 0, s), mutpb) : 0;
+    const int wave_any = (__ballot(any & ANY_COLOR) ? ANY_COLOR : 0) | (__ballot(any & ANY_XY) ? ANY_XY : 0) |
+                         (__ballot(any & ANY_AB) ? ANY_AB : 0) | (__ballot(any & ANY_T) ? ANY_T : 0);
+    if ((threadIdx.x & 63) == 0 && wave_any) atomicOr(&tflags[t], wave_any);
+}
+
+hipError_t launch_sa_flags(hipStream_t st, int64_t pos0, int n_tries, int tries, uint64_t seed, float mutpb, int N,
+                           int* tflags) {
+    const int nch = (N + SA_VT - 1) / SA_VT;
+    hipError_t e = hipMemsetAsync(tflags, 0, sizeof(int) * (size_t)n_tries, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(sa_flags_kernel, dim3((unsigned)((int64_t)n_tries * nch)), dim3(SA_VT), 0, st, pos0, tries,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), mutpb, N, nch, tflags);
+    return hipGetLastError();
+}
+
+// pass 2: mutate each splat of the current state into neighbour o, its raster
+// record, and its size exp(a)exp(b) for the swap
+__global__ void __launch_bounds__(SA_VT)
+sa_mutate_kernel(const SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, GaParamsDev prm, uint32_t k0,
+                 uint32_t k1, int N, int nch, const int* __restrict__ tflags, const float* __restrict__ curr,
+                 float* __restrict__ off, float* __restrict__ sizes, SplatRec* __restrict__ recs, int H, int W,
+                 float k_sigma) {
+    const int o = blockIdx.x / nch, s = (blockIdx.x % nch) * SA_VT + threadIdx.x;
+    if (o >= sl->live || s >= N) return;
+    const SaTry t = sa_try(*sl, sit, o, prm);
+    const Rng rng{k0, k1, (uint32_t)t.gen};
+    const GaDrawsDev d{};
+    const SaLoopDev& sv = *sl;
+    const Fallback fb = fallbacks(d, rng, t.og, o, N, tflags[sv.pos + o - (int64_t)sv.first_it * sv.tries]);
+    const MaskU u = mask_draws(d, rng, t.og, 0, s);
+    const NormD nd = normal_draws(d, rng, t.og, 0, s, N);
+    float g[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) g[c] = curr[(int64_t)s * 9 + c];
+    mutate_row(g, u, nd, fb, s, prm);
+    const int64_t os = (int64_t)o * N + s;
+#pragma unroll
+    for (int c = 0; c < 9; ++c) off[os * 9 + c] = g[c];
+    sizes[os] = expf(g[2]) * expf(g[3]);
+    float row[9];
+    encode_row(g, row);
+    recs[os] = make_rec(preprocess_row(row, H, W, k_sigma));
+}
+
+// genetic.py:79-91 on neighbour o: the pick-th later splat bigger than a random
+// splat i trades rows (and raster records) with it
+__global__ void __launch_bounds__(1024)
+sa_swap_kernel(const SaLoopDev* __restrict__ sl, uint32_t k0, uint32_t k1, int N, const float* __restrict__ sizes,
+               float* __restrict__ off, SplatRec* __restrict__ recs) {
+    __shared__ int s_scan[16], s_count, s_j;
+    const int o = blockIdx.x, tid = threadIdx.x;
+    const SaLoopDev& sv = *sl;
+    if (o >= sv.live || N < 2) return;
+    const int64_t g = sv.pos + o;
+    const uint32_t og = (uint32_t)(g % sv.tries);
+    const Rng rng{k0, k1, (uint32_t)(g / sv.tries)};
+    const float* __restrict__ sz = sizes + (int64_t)o * N;
+    const int i = (int)(rng.block(S_IND, og, 4).x % (uint32_t)(N - 1));
+    const float sizei = sz[i];
+    const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+    int cnt = 0;
+    for (int s = tid; s < N; s += blockDim.x) cnt += (s > i) && (sz[s] > sizei);
+    for (int k = 32; k > 0; k >>= 1) cnt += __shfl_xor(cnt, k);
+    if (lane == 0) s_scan[w] = cnt;
+    if (tid == 0) s_j = -1;
+    __syncthreads();
+    if (tid == 0) {
+        int tot = 0;
+        for (int k = 0; k < nw; ++k) tot += s_scan[k];
+        s_count = tot;
+    }
+    __syncthreads();
+    const int count = s_count;
+    if (count == 0) return;
+    int pick = (int)((double)u01(rng.block(S_IND, og, 5).x) * (double)count);
+    if (pick > count - 1) pick = count - 1;
+    int seen = 0;
+    for (int base = 0; base < N; base += blockDim.x) {   // the (pick+1)-th candidate in splat order
+        const int s = base + tid;
+        const bool c = s < N && s > i && sz[s] > sizei;
+        const uint64_t bal = __ballot(c);
+        const int inwave = __popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+        __syncthreads();
+        if (lane == 0) s_scan[w] = __popcll(bal);
+        __syncthreads();
+        int before = seen;
+        for (int k = 0; k < w; ++k) before += s_scan[k];
+        if (c && before + inwave == pick) s_j = s;
+        int tot = 0;
+        for (int k = 0; k < nw; ++k) tot += s_scan[k];
+        seen += tot;
+        __syncthreads();
+        if (s_j >= 0) break;
+    }
+    const int j = s_j;
+    if (j < 0) return;
+    float* __restrict__ O = off + (int64_t)o * N * 9;
+    if (tid < 9) {
+        const float a = O[(int64_t)i * 9 + tid], b = O[(int64_t)j * 9 + tid];
+        O[(int64_t)i * 9 + tid] = b;
+        O[(int64_t)j * 9 + tid] = a;
+    } else if (tid >= 64 && tid < 64 + 4) {           // a record is a function of its row alone
+        float4* ri = reinterpret_cast<float4*>(recs + (int64_t)o * N + i) + (tid - 64);
+        float4* rj = reinterpret_cast<float4*>(recs + (int64_t)o * N + j) + (tid - 64);
+        const float4 a = *ri, b = *rj;
+        *ri = b;
+        *rj = a;
+    }
+}
+
+hipError_t launch_sa_mutate(hipStream_t st, const SaLoopDev* sl, const SaItDev* sit, const GaParamsDev& prm,
+                            uint64_t seed, int N, int cap, const int* tflags, const float* curr, float* off,
+                            float* sizes, SplatRec* recs, int H, int W, float k_sigma) {
+    const int nch = (N + SA_VT - 1) / SA_VT;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    hipLaunchKernelGGL(sa_mutate_kernel, dim3(cap * nch), dim3(SA_VT), 0, st, sl, sit, prm, k0, k1, N, nch, tflags,
+                       curr, off, sizes, recs, H, W, k_sigma);
+    hipLaunchKernelGGL(sa_swap_kernel, dim3(cap), dim3(1024), 0, st, sl, k0, k1, N, sizes, off, recs);
+    return hipGetLastError();
+}
+
+__global__ void sa_begin_kernel(SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it, int cap,
+                                int width) {
+    SaLoopDev s = *sl;
+    s.pos = pos;
+    s.end = end;
+    s.tries = tries;
+    s.first_it = first_it;
+    s.cap = cap;
+    s.width = width;
+    s.acc_j = -1;
+    s.new_best = 0;
+    s.live = sa_width(s);
+    *sl = s;
+}
+
+// The end of a round, one workgroup: the neighbours' fitness (finalize_wave, the
+// bits of finalize_kernel), then annealing.py:130-150 over them in try order by
+// one thread, then the workgroup installs the accepted neighbour.  Same arithmetic as the
 // host loop (ggs/annealing.py): dE in float64 from the float32 energies, the
 // Metropolis test u < exp(-dE/T) (device exp; the host's math.exp agrees to the
 // last ulp in all but rare cases, and u would have to fall between the two),
 // the 1e-12 best margin.
-__global__ void __launch_bounds__(256)
-sa_accept_kernel(SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, const float* __restrict__ fits,
-                 uint64_t seed, double* __restrict__ curves, float* __restrict__ curr, float* __restrict__ best,
-                 const float* __restrict__ nb, int N, SplatRec* __restrict__ cur_recs,
-                 const SplatRec* __restrict__ nb_recs, float* __restrict__ cur_part,
-                 const float* __restrict__ nb_part, int nslots) {
+__global__ void __launch_bounds__(1024)
+sa_accept_kernel(SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, SaRoundDev r) {
     __shared__ int s_j, s_nb;
+    __shared__ float fits[SMAX];
+    const int N = r.N;
+    {
+        const int live = sl->live, nw = blockDim.x >> 6;
+        for (int b = threadIdx.x >> 6; b < live; b += nw) {
+            const float v = finalize_wave(r.partials, r.wpartials, r.nslots, r.mode, r.hw, b);
+            if ((threadIdx.x & 63) == 0) {
+                fits[b] = v;
+                r.fits_out[b] = v;
+            }
+        }
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
+        const uint64_t seed = r.seed;
+        double* __restrict__ curves = r.curves;
         SaLoopDev s = *sl;
         int jacc = -1, nbest = 0;
         if (s.live > 0) {
@@ -613,18 +798,38 @@ sa_accept_kernel(SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, co
     __syncthreads();
     const int j = s_j;
     if (j < 0) return;
-    const int64_t n9 = (int64_t)N * 9;
-    const float* src = nb + j * n9;
-    for (int64_t i = threadIdx.x; i < n9; i += blockDim.x) {
-        const float v = src[i];
-        curr[i] = v;
-        if (s_nb) best[i] = v;
+    float* __restrict__ curr = r.curr;
+    float* __restrict__ best = r.best;
+    // install: 16-B copies (the genome is 36 N bytes: N % 4 floats of tail)
+    const int64_t n9 = (int64_t)N * 9, n4 = n9 >> 2;
+    const float* src = r.nb + j * n9;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* c4 = reinterpret_cast<float4*>(curr);
+    float4* b4 = reinterpret_cast<float4*>(best);
+    const bool nbst = s_nb;
+    if (((j * n9) & 3) == 0) {
+        for (int64_t i = threadIdx.x; i < n4; i += blockDim.x) {
+            const float4 v = s4[i];
+            c4[i] = v;
+            if (nbst) b4[i] = v;
+        }
+        for (int64_t i = 4 * n4 + threadIdx.x; i < n9; i += blockDim.x) {
+            curr[i] = src[i];
+            if (nbst) best[i] = src[i];
+        }
+    } else {
+        for (int64_t i = threadIdx.x; i < n9; i += blockDim.x) {
+            const float v = src[i];
+            curr[i] = v;
+            if (nbst) best[i] = v;
+        }
     }
-    if (cur_recs) {         // incremental evaluation keeps the state's records and partials
-        const float4* rs = reinterpret_cast<const float4*>(nb_recs + j * (int64_t)N);
-        float4* rd = reinterpret_cast<float4*>(cur_recs);
+    if (r.cur_recs) {       // incremental evaluation keeps the state's records and partials
+        const float4* rs = reinterpret_cast<const float4*>(r.nb_recs + j * (int64_t)N);
+        float4* rd = reinterpret_cast<float4*>(r.cur_recs);
         for (int64_t i = threadIdx.x; i < 4 * (int64_t)N; i += blockDim.x) rd[i] = rs[i];
-        for (int i = threadIdx.x; i < nslots; i += blockDim.x) cur_part[i] = nb_part[(int64_t)j * nslots + i];
+        for (int i = threadIdx.x; i < r.nslots; i += blockDim.x)
+            r.cur_part[i] = r.partials[(int64_t)j * r.nslots + i];
     }
 }
 
@@ -634,11 +839,8 @@ hipError_t launch_sa_begin(hipStream_t st, SaLoopDev* sl, int64_t pos, int64_t e
     return hipGetLastError();
 }
 
-hipError_t launch_sa_accept(hipStream_t st, SaLoopDev* sl, const SaItDev* sit, const float* fits, uint64_t seed,
-                            double* curves, float* curr, float* best, const float* nb, int N, SplatRec* cur_recs,
-                            const SplatRec* nb_recs, float* cur_part, const float* nb_part, int nslots) {
-    hipLaunchKernelGGL(sa_accept_kernel, dim3(1), dim3(256), 0, st, sl, sit, fits, seed, curves, curr, best, nb,
-                       N, cur_recs, nb_recs, cur_part, nb_part, nslots);
+hipError_t launch_sa_accept(hipStream_t st, SaLoopDev* sl, const SaItDev* sit, const SaRoundDev& r) {
+    hipLaunchKernelGGL(sa_accept_kernel, dim3(1), dim3(1024), 0, st, sl, sit, r);
     return hipGetLastError();
 }
 

@@ -107,15 +107,40 @@ struct SaItDev {                // one iteration of the chunk
     float pad_[2];
     double T;                   // temperature (annealing.py:29-44)
 };
-// One device round's acceptance walk + install of the accepted neighbour
-// (genome; records and strip partials too when `recs_too`, for the incremental
-// path); curves[(it - first_it)*2 + {0,1}] = best, current after each iteration.
-hipError_t launch_sa_accept(hipStream_t st, SaLoopDev* sl, const SaItDev* sit, const float* fits, uint64_t seed,
-                            double* curves, float* curr, float* best, const float* nb, int N, SplatRec* cur_recs,
-                            const SplatRec* nb_recs, float* cur_part, const float* nb_part, int nslots);
-// Start a chunk: pos/end/tries/first_it, and the first round's width.
+// The end of a device round (one workgroup): the neighbours' fitness from their
+// strip partials (finalize_wave), the acceptance walk, the install of the
+// accepted neighbour (genome; records and strip partials too when cur_recs is
+// set, for the incremental path), curves[(it - first_it)*2 + {0,1}] = best,
+// current after each iteration, and the next round's mask-group flags.
+struct SaRoundDev {
+    const float* partials;      // [cap][nslots] the round's strip partials
+    const float* wpartials;     // [nslots] plan weight sums
+    int nslots, mode, N;
+    double hw;
+    float* fits_out;            // [cap] the round's energies (kept for inspection)
+    uint64_t seed;
+    float mutpb;
+    double* curves;
+    float *curr, *best;         // [N][9] state
+    const float* nb;            // [cap][N][9] the round's neighbours
+    SplatRec* cur_recs;         // incremental only (else null)
+    const SplatRec* nb_recs;
+    float* cur_part;
+};
+hipError_t launch_sa_accept(hipStream_t st, SaLoopDev* sl, const SaItDev* sit, const SaRoundDev& r);
+// Start a chunk: pos/end/tries/first_it and the first round's width.
 hipError_t launch_sa_begin(hipStream_t st, SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it,
                            int cap, int width);
+// Mask-group flags of the chunk's n_tries tries from pos0 (state-independent):
+// tflags [n_tries], zeroed here.
+hipError_t launch_sa_flags(hipStream_t st, int64_t pos0, int n_tries, int tries, uint64_t seed, float mutpb, int N,
+                           int* tflags);
+// The round's neighbours (Philox draws; the bits of ga_variation_kernel's
+// mutate-only mode) with their raster records: tflags of the chunk's tries,
+// sizes [cap][N] scratch, off [cap][N][9], recs [cap][N].
+hipError_t launch_sa_mutate(hipStream_t st, const SaLoopDev* sl, const SaItDev* sit, const GaParamsDev& prm,
+                            uint64_t seed, int N, int cap, const int* tflags, const float* curr, float* off,
+                            float* sizes, SplatRec* recs, int H, int W, float k_sigma);
 // The acceptance uniform of try (it, k): Philox4x32-10 keyed by seed, 53-bit double
 // in [0, 1).  Host and device compute the same bits.
 double sa_accept_uniform(uint64_t seed, uint32_t it, uint32_t k);

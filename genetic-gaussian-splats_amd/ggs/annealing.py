@@ -32,6 +32,7 @@ with the device backend replays the same trajectory on the host
 from __future__ import annotations
 
 import math
+import time
 from typing import Callable, Optional
 
 import numpy as np
@@ -155,7 +156,8 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
             return _finish(best, best_fit, curr, curr_fit, curves, stats, prefix, loss_png_path,
                            loss_csv_path, loss_log_y, return_state)
         acc_rate = 0.0                 # EWMA of the per-try acceptance rate
-        stats = {"evaluated": 0, "tries": 0, "launches": 0}
+        stats = {"evaluated": 0, "tries": 0, "launches": 0, "accepted": 0}
+        t_loop = time.perf_counter()
         bar = range(iterations)
         if progress:
             try:
@@ -194,6 +196,7 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
                             curr_fit = e_new
                             e_curr = curr_fit
                             accepted_any = True
+                            stats["accepted"] += 1
                         new_best = e_curr + 1e-12 < best_fit               # annealing.py:148-150
                         if new_best:
                             best_fit = e_curr
@@ -215,6 +218,7 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
         finally:
             if hasattr(bar, "close"):
                 bar.close()
+        stats["loop_s"] = time.perf_counter() - t_loop
         best, curr = prop.best(), prop.current()
         stats.update(prop.stats())
     finally:
@@ -243,6 +247,7 @@ def _device_loop(sa, curves, iterations, tries, sched, temp0, width, chunk, prog
             pass
     st = sa.loop_state()
     it = 0
+    t0 = time.perf_counter()
     try:
         while it < iterations:
             n = min(max(1, int(chunk)), iterations - it)
@@ -271,7 +276,7 @@ def _device_loop(sa, curves, iterations, tries, sched, temp0, width, chunk, prog
         if bar is not None:
             bar.close()
     stats = {"evaluated": st["evaluated"], "tries": it * tries, "launches": st["rounds"],
-             "accepted": st["accepted"]}
+             "accepted": st["accepted"], "loop_s": time.perf_counter() - t0}
     return st["best_fit"], st["current_fit"], stats
 
 

@@ -266,7 +266,9 @@ def test_device_loop_width_invariant_low_temperature():
     for b, f, st in outs[1:]:
         np.testing.assert_array_equal(b, outs[0][0])
         assert f == outs[0][1] and st["curves"] == outs[0][2]["curves"]
-    assert outs[0][2]["stats"]["launches"] < 40      # rounds held more than one iteration
+    # a round ends at an acceptance or after its width of tries, across iteration ends
+    st13 = outs[2][2]["stats"]
+    assert st13["launches"] <= st13["accepted"] + -(-200 // 13)
     assert outs[1][2]["stats"]["evaluated"] == outs[1][2]["stats"]["launches"]   # width 1
     b, f, _ = outs[0]
     assert float(ggs.fitness(b[None], t, H, W, 3.0, weight_mask=m)[0]) == f

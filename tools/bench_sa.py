@@ -1,7 +1,9 @@
 """SA throughput at BASELINE configs[4] (run_sags.py: 2048x2048, 4096 splats,
 SA_TRIES_PER_ITER=8, MUTPB=0.05, T0=1e-3 cosine): iterations/s of
-ggs.annealing.simulated_annealing over the SA loop alone (setup — target prep,
-importance mask, initial evaluation — is timed separately and subtracted):
+ggs.annealing.simulated_annealing over the SA loop alone (stats["loop_s"]: the
+iteration loop's own wall time; setup — target prep, importance mask, initial
+evaluation, ~0.9 s at 2048^2 — is reported separately.  Round 1 subtracted a
+separately timed setup run instead, and its ±50 ms jitter swamped the ~0.2 s loop):
 * host / sequential: numpy mutation, one host-API launch per try (the
   reference's schedule);
 * host / speculative: numpy mutation, batched tries;
@@ -68,16 +70,13 @@ for name, spec, backend, inc, loop in variants:
     iters = a.dev_iters if loop == "device" else a.iters
     reps = a.repeat if loop == "device" else 1
     run(2)                                           # warm-up
-    t0 = time.perf_counter()
-    run(0)                                           # setup only
-    t_setup = time.perf_counter() - t0
     rates = []
     for _ in range(reps):
         ev["s"] = 0.0
         t0 = time.perf_counter()
         best, fit, st = run(iters)
-        dt = time.perf_counter() - t0 - t_setup
-        rates.append(iters / dt)
+        t_setup = time.perf_counter() - t0 - st["stats"]["loop_s"]
+        rates.append(iters / st["stats"]["loop_s"])
     dt = iters / sorted(rates)[len(rates) // 2]
     res[name] = {"iters_per_s": round(iters / dt, 2), "ms_per_iter": round(dt / iters * 1e3, 2),
                  "iters": iters, "runs_iters_per_s": [round(r, 1) for r in rates],
