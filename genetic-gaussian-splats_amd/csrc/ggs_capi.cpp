@@ -22,9 +22,6 @@
 
 #include "ggs_internal.h"
 
-#ifndef GGS_GA_FUSED_PREP
-#define GGS_GA_FUSED_PREP 1   // prep inside the variation kernel (A/B: 3,917 vs 3,884 gens/s separate)
-#endif
 
 namespace ggs {
 namespace {
@@ -102,7 +99,7 @@ int ensure_pinned(PinBuf& b, size_t bytes) {
 // Per-(device, stream) scratch used by one render/fitness pipeline.
 struct Workspace {
     hipStream_t stream = nullptr;
-    DevBuf recs, partials, wpartials, order, plan;
+    DevBuf recs, bnds, partials, wpartials, order, plan;
     int order_H = -1, order_W = -1;   // (H, W) the tile order was built for
     uint64_t plan_key = 0;            // inputs the plan was built from (0: none / volatile)
 };
@@ -322,6 +319,7 @@ int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N,
     const int nTiles = raster_tiles(H, W, &nTX);
     int rc;
     if ((rc = ensure(w->recs, sizeof(SplatRec) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
+    if ((rc = ensure(w->bnds, sizeof(int4) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
     // one partial per (candidate, tile, 16-column strip)
     if ((rc = ensure(w->partials, sizeof(float) * 4 * (size_t)(B * nTiles), st))) return rc;
     if ((rc = ensure(w->wpartials, sizeof(float) * 4 * (size_t)nTiles, st))) return rc;
@@ -346,17 +344,19 @@ int run_fitness_planned(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B
     const int nTiles = raster_tiles(H, W, &nTX);
     int rc;
     if ((rc = ensure(w->recs, sizeof(SplatRec) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
+    if ((rc = ensure(w->bnds, sizeof(int4) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
     if ((rc = ensure(w->partials, sizeof(float) * 4 * (size_t)(B * nTiles), st))) return rc;
     if ((rc = ensure_tile_order(w, H, W, st))) return rc;
     SplatRec* recs = (SplatRec*)w->recs.p;
     {
         ProfScope ps(st, 0);
-        GGS_HIP(launch_prep(st, true, d_gen, B * N, C, H, W, k, recs, nullptr, nullptr, nullptr));
+        GGS_HIP(launch_prep(st, true, d_gen, B * N, C, H, W, k, recs, (int4*)w->bnds.p, nullptr, nullptr, nullptr));
     }
     const float bg[3] = {1.f, 1.f, 1.f};  // fitness renders with the default background (fitness.py:15)
     {
         ProfScope ps(st, 1);
-        GGS_HIP(launch_raster(st, 1, recs, (int)B, N, H, W, bg, nullptr, plan, (float*)w->partials.p,
+        GGS_HIP(launch_raster(st, 1, recs, (const int4*)w->bnds.p, (int)B, N, H, W, bg, nullptr, plan,
+                              (float*)w->partials.p,
                               (const int*)w->order.p));
     }
     {
@@ -373,15 +373,16 @@ int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, 
     Workspace* w = workspace_for(c, st);
     int rc;
     if ((rc = ensure(w->recs, sizeof(SplatRec) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
+    if ((rc = ensure(w->bnds, sizeof(int4) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
     if ((rc = ensure_tile_order(w, H, W, st))) return rc;
     SplatRec* recs = (SplatRec*)w->recs.p;
     {
         ProfScope ps(st, 0);
-        GGS_HIP(launch_prep(st, false, d_gen, B * N, C, H, W, k, recs, nullptr, nullptr, nullptr));
+        GGS_HIP(launch_prep(st, false, d_gen, B * N, C, H, W, k, recs, (int4*)w->bnds.p, nullptr, nullptr, nullptr));
     }
     {
         ProfScope ps(st, 1);
-        GGS_HIP(launch_raster(st, 0, recs, (int)B, N, H, W, bg, d_img, nullptr, nullptr,
+        GGS_HIP(launch_raster(st, 0, recs, (const int4*)w->bnds.p, (int)B, N, H, W, bg, d_img, nullptr, nullptr,
                               (const int*)w->order.p));
     }
     return GGS_OK;
@@ -478,7 +479,7 @@ void ggs_shutdown(void) {
         (void)hipStreamSynchronize(c->stream);
         for (auto& w : c->ws) {
             if (w->stream) (void)hipStreamSynchronize(w->stream);
-            for (DevBuf* b : {&w->recs, &w->partials, &w->wpartials, &w->order, &w->plan})
+            for (DevBuf* b : {&w->recs, &w->bnds, &w->partials, &w->wpartials, &w->order, &w->plan})
                 if (b->p) (void)hipFree(b->p);
         }
         for (DevBuf* b : {&c->gen, &c->out, &c->target, &c->mask})
@@ -764,7 +765,7 @@ static int stage_call(bool encode, const float* in, int64_t S, int32_t C, int32_
     GGS_HIP(hipMalloc(&dout.p, ob));
     GGS_HIP(hipMemcpyAsync(din.p, in, ib, hipMemcpyHostToDevice, st));
     float* o = (float*)dout.p;
-    GGS_HIP(launch_prep(st, encode, (const float*)din.p, S, C, H, W, k, nullptr, f9 ? o : nullptr,
+    GGS_HIP(launch_prep(st, encode, (const float*)din.p, S, C, H, W, k, nullptr, nullptr, f9 ? o : nullptr,
                         f9 ? (int*)(o + 9 * S) : nullptr, enc9 ? o : nullptr));
     GGS_HIP(hipStreamSynchronize(st));
     if (f9) {
@@ -865,7 +866,7 @@ struct GaSession {
     int P = 0, N = 0, cur = 0, nTiles = 0;
     DevBuf pop[2], fits[2], off, off_fits, src, target, mask, best_ind, best_fit, best_src,
         best_upd, curves, draws;
-    DevBuf recs, partials, plan, wpart, order;   // the generation's fused pipeline
+    DevBuf recs, bnds, partials, plan, wpart, order;   // the generation's fused pipeline
     int64_t n_curves = 0, curves_cap = 0;
     void* comm = nullptr;          // ggs_ga_set_comm: offspring fitness sharded over ranks
     int nranks = 1, rank = 0;
@@ -963,22 +964,12 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     const ggs_ga_config& c = s->cfg;
     // five launches per generation: variation (+ prep of the offspring), raster,
     // finalize, survivors, gather
-#if GGS_GA_FUSED_PREP
-    {
+    {   // the offspring's raster records are prepped inside the variation kernel
         ProfScope ps(s->st, 0);
         GGS_HIP(launch_ga_variation(s->st, (const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
                                     P, N, prm, d, c.seed, gen, (float*)s->off.p, P, (SplatRec*)s->recs.p,
-                                    c.H, c.W, c.k_sigma));
+                                    (int4*)s->bnds.p, c.H, c.W, c.k_sigma));
     }
-#else
-    GGS_HIP(launch_ga_variation(s->st, (const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p, P, N,
-                                prm, d, c.seed, gen, (float*)s->off.p, P));
-    {
-        ProfScope ps(s->st, 0);
-        GGS_HIP(launch_prep(s->st, true, (const float*)s->off.p, (int64_t)P * N, 9, c.H, c.W, c.k_sigma,
-                            (SplatRec*)s->recs.p, nullptr, nullptr, nullptr));
-    }
-#endif
     const float bg[3] = {1.f, 1.f, 1.f};
     // this rank's contiguous shard of the offspring (all of them on one GPU);
     // every rank bred all P offspring above with the same draws
@@ -987,7 +978,8 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     if (nb > 0) {
         {
             ProfScope ps(s->st, 1);
-            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->recs.p + (int64_t)b0 * N, nb, N, c.H, c.W, bg,
+            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->recs.p + (int64_t)b0 * N,
+                                  (const int4*)s->bnds.p + (int64_t)b0 * N, nb, N, c.H, c.W, bg,
                                   nullptr, (const float4*)s->plan.p, (float*)s->partials.p,
                                   (const int*)s->order.p));
         }
@@ -1027,7 +1019,7 @@ struct SaSession {
     int N = 0, cap = 0, last_n = 0, nTiles = 0;
     bool incremental = false;   // measured slower at every SA config tried
     DevBuf curr, best, nb, nb_fits, target, mask, draws;
-    DevBuf cur_recs, nb_recs, cur_part, nb_part, dirty, plan, wpart, order, counters;
+    DevBuf cur_recs, nb_recs, nb_bnds, cur_part, nb_part, dirty, plan, wpart, order, counters;
     DevBuf loop, sit, curves;       // device SA loop (ggs_sa_run): state, per-iteration table, curves
     DevBuf flags, sizes;            // ... and its mutation scratch (per-try mask-group flags, splat sizes)
     float* h_fits = nullptr;        // pinned
@@ -1039,7 +1031,7 @@ struct SaSession {
 
 void sa_free(SaSession* s) {
     for (DevBuf* b : {&s->curr, &s->best, &s->nb, &s->nb_fits, &s->target, &s->mask, &s->draws,
-                      &s->cur_recs, &s->nb_recs, &s->cur_part, &s->nb_part, &s->dirty, &s->plan,
+                      &s->cur_recs, &s->nb_recs, &s->nb_bnds, &s->cur_part, &s->nb_part, &s->dirty, &s->plan,
                       &s->wpart, &s->order, &s->counters, &s->loop, &s->sit, &s->curves, &s->flags, &s->sizes})
         if (b->p) (void)hipFree(b->p);
     if (s->h_loop) (void)hipHostFree(s->h_loop);
@@ -1050,12 +1042,13 @@ void sa_free(SaSession* s) {
 
 // prep -> [dirty] -> raster -> finalize for n genomes G; records / partials / fitness
 // land in recs / part / fits.  dirty != null: incremental against the current state.
-int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, float* part, float* fits, bool dirty,
+// bnds: the records' cull bounds (scratch for the current state's evaluation).
+int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, int4* bnds, float* part, float* fits, bool dirty,
             bool have_recs = false) {
     const ggs_ga_config& c = s->cfg;
     if (!have_recs) {
         ProfScope ps(s->st, 0);
-        GGS_HIP(launch_prep(s->st, true, G, (int64_t)n * s->N, 9, c.H, c.W, c.k_sigma, recs, nullptr,
+        GGS_HIP(launch_prep(s->st, true, G, (int64_t)n * s->N, 9, c.H, c.W, c.k_sigma, recs, bnds, nullptr,
                             nullptr, nullptr));
     }
     if (dirty)
@@ -1064,7 +1057,7 @@ int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, float* part, fl
     const float bg[3] = {1.f, 1.f, 1.f};
     {
         ProfScope ps(s->st, 1);
-        GGS_HIP(launch_raster(s->st, 1, recs, n, s->N, c.H, c.W, bg, nullptr, (const float4*)s->plan.p, part,
+        GGS_HIP(launch_raster(s->st, 1, recs, bnds, n, s->N, c.H, c.W, bg, nullptr, (const float4*)s->plan.p, part,
                               (const int*)s->order.p, dirty ? (const unsigned char*)s->dirty.p : nullptr,
                               (const float*)s->cur_part.p));
     }
@@ -1100,7 +1093,7 @@ void ga_fill_log_bounds(ggs_ga_config* c) {   // utils.py:38-39 when the caller 
 void ga_free(GaSession* s) {
     for (DevBuf* b : {&s->pop[0], &s->pop[1], &s->fits[0], &s->fits[1], &s->off, &s->off_fits, &s->src,
                       &s->target, &s->mask, &s->best_ind, &s->best_fit, &s->best_src, &s->best_upd,
-                      &s->curves, &s->draws, &s->recs, &s->partials, &s->plan, &s->wpart, &s->order})
+                      &s->curves, &s->draws, &s->recs, &s->bnds, &s->partials, &s->plan, &s->wpart, &s->order})
         if (b->p) (void)hipFree(b->p);
     if (s->st) (void)hipStreamDestroy(s->st);
 }
@@ -1150,6 +1143,7 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     s->nTiles = raster_tiles(c.H, c.W, &nTX);
     const size_t slots = 4 * (size_t)s->nTiles;
     if ((rc = ensure(s->recs, sizeof(SplatRec) * std::max<size_t>((size_t)s->P * s->N, 1), s->st)) ||
+        (rc = ensure(s->bnds, sizeof(int4) * std::max<size_t>((size_t)s->P * s->N, 1), s->st)) ||
         (rc = ensure(s->partials, sizeof(float) * slots * s->P, s->st)) ||
         (rc = ensure(s->plan, plan_bytes(c.H, c.W), s->st)) || (rc = ensure(s->wpart, sizeof(float) * slots, s->st)) ||
         (rc = ensure(s->order, sizeof(int) * (size_t)raster_order_len(c.H, c.W), s->st)))
@@ -1295,6 +1289,7 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
         (rc = ensure(s->target, sizeof(float) * 3 * hw, s->st)) ||
         (mask_hw && (rc = ensure(s->mask, sizeof(float) * hw, s->st))) ||
         (rc = ensure(s->cur_recs, rb, s->st)) || (rc = ensure(s->nb_recs, rb * s->cap, s->st)) ||
+        (rc = ensure(s->nb_bnds, rb / 4 * s->cap, s->st)) ||
         (rc = ensure(s->cur_part, sizeof(float) * slots, s->st)) ||
         (rc = ensure(s->nb_part, sizeof(float) * slots * s->cap, s->st)) ||
         (rc = ensure(s->dirty, slots * s->cap, s->st)) || (rc = ensure(s->plan, plan_bytes(cfg->H, cfg->W), s->st)) ||
@@ -1320,7 +1315,8 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
                     cfg->fitness_mode, cfg->boost_beta, cfg->H, cfg->W, (float4*)s->plan.p,
                     (float*)s->wpart.p) != hipSuccess)
         return bail(fail(GGS_EHIP, "plan launch failed"));
-    if ((rc = sa_eval(s.get(), (const float*)s->curr.p, 1, (SplatRec*)s->cur_recs.p, (float*)s->cur_part.p,
+    if ((rc = sa_eval(s.get(), (const float*)s->curr.p, 1, (SplatRec*)s->cur_recs.p, (int4*)s->nb_bnds.p,
+                      (float*)s->cur_part.p,
                       (float*)s->nb_fits.p, false)))
         return bail(rc);
     if (hipMemcpyAsync(s->h_fits, s->nb_fits.p, sizeof(float), hipMemcpyDeviceToHost, s->st) ||
@@ -1363,9 +1359,11 @@ int ggs_sa_propose(void* handle, int32_t it, int32_t total_iters, int32_t first_
         ProfScope ps(s->st, 0);
         GGS_HIP(launch_ga_variation(s->st, (const float*)s->curr.p, nullptr, 1, s->N, prm, d, s->cfg.seed, it,
                                     (float*)s->nb.p, n, fuse_prep ? (SplatRec*)s->nb_recs.p : nullptr,
+                                    (int4*)s->nb_bnds.p,
                                     s->cfg.H, s->cfg.W, s->cfg.k_sigma));
     }
-    if ((rc = sa_eval(s, (const float*)s->nb.p, n, (SplatRec*)s->nb_recs.p, (float*)s->nb_part.p,
+    if ((rc = sa_eval(s, (const float*)s->nb.p, n, (SplatRec*)s->nb_recs.p, (int4*)s->nb_bnds.p,
+                      (float*)s->nb_part.p,
                       (float*)s->nb_fits.p, s->incremental, fuse_prep)))
         return rc;
     GGS_HIP(hipMemcpyAsync(s->h_fits, s->nb_fits.p, sizeof(float) * n, hipMemcpyDeviceToHost, s->st));
@@ -1462,7 +1460,7 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
             ProfScope ps(s->st, 0);
             GGS_HIP(launch_sa_mutate(s->st, loop, sit, prm, c.seed, s->N, s->cap, (int*)s->flags.p,
                                      (const float*)s->curr.p, (float*)s->nb.p, (float*)s->sizes.p,
-                                     (SplatRec*)s->nb_recs.p, c.H, c.W, c.k_sigma));
+                                     (SplatRec*)s->nb_recs.p, (int4*)s->nb_bnds.p, c.H, c.W, c.k_sigma));
         }
         if (s->incremental)
             GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, (const float*)s->nb.p,
@@ -1470,7 +1468,8 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
                                  c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p, live));
         {
             ProfScope ps(s->st, 1);
-            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->nb_recs.p, s->cap, s->N, c.H, c.W, bg, nullptr,
+            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->nb_recs.p, (const int4*)s->nb_bnds.p, s->cap, s->N,
+                                  c.H, c.W, bg, nullptr,
                                   (const float4*)s->plan.p, (float*)s->nb_part.p, (const int*)s->order.p,
                                   s->incremental ? (const unsigned char*)s->dirty.p : nullptr,
                                   (const float*)s->cur_part.p, live));

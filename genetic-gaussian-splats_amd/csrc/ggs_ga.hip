@@ -199,7 +199,8 @@ template <int VT>
 __global__ void __launch_bounds__(VT)
 ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fits, int P, int N,
                     GaParamsDev prm, GaDrawsDev d, uint32_t k0, uint32_t k1, int gen,
-                    float* __restrict__ off, SplatRec* __restrict__ recs, int H, int W, float k_sigma,
+                    float* __restrict__ off, SplatRec* __restrict__ recs, int4* __restrict__ bnds, int H, int W,
+                    float k_sigma,
                     const SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit) {
     __shared__ int s_a, s_b, s_cx;
     __shared__ float s_sizei;
@@ -341,7 +342,9 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
         for (int s = tid; s < N; s += VT) {
             float row[9];
             encode_row(O + (int64_t)s * 9, row);
-            recs[(int64_t)o * N + s] = make_rec(preprocess_row(row, H, W, k_sigma));
+            const SplatRec r = make_rec(preprocess_row(row, H, W, k_sigma));
+            recs[(int64_t)o * N + s] = r;
+            bnds[(int64_t)o * N + s] = rec_bounds(r);
         }
     }
 }
@@ -522,14 +525,14 @@ ga_gather_kernel(const float* __restrict__ pop, const float* __restrict__ off, i
 // ---------------------------------------------------------------------------
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
-                               float* off, int n_off, SplatRec* recs, int H, int W, float k_sigma,
+                               float* off, int n_off, SplatRec* recs, int4* bnds, int H, int W, float k_sigma,
                                const SaLoopDev* sl, const SaItDev* sit) {
     if (n_off < 64 && N >= 1024)
         hipLaunchKernelGGL(ga_variation_kernel<1024>, dim3(n_off), dim3(1024), 0, st, pop, fits, P, N, prm, d,
-                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma, sl, sit);
+                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, bnds, H, W, k_sigma, sl, sit);
     else
         hipLaunchKernelGGL(ga_variation_kernel<256>, dim3(n_off), dim3(256), 0, st, pop, fits, P, N, prm, d,
-                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, H, W, k_sigma, sl, sit);
+                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, bnds, H, W, k_sigma, sl, sit);
     return hipGetLastError();
 }
 
@@ -614,8 +617,8 @@ hipError_t launch_sa_flags(hipStream_t st, int64_t pos0, int n_tries, int tries,
 __global__ void __launch_bounds__(SA_VT)
 sa_mutate_kernel(const SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, GaParamsDev prm, uint32_t k0,
                  uint32_t k1, int N, int nch, const int* __restrict__ tflags, const float* __restrict__ curr,
-                 float* __restrict__ off, float* __restrict__ sizes, SplatRec* __restrict__ recs, int H, int W,
-                 float k_sigma) {
+                 float* __restrict__ off, float* __restrict__ sizes, SplatRec* __restrict__ recs,
+                 int4* __restrict__ bnds, int H, int W, float k_sigma) {
     const int o = blockIdx.x / nch, s = (blockIdx.x % nch) * SA_VT + threadIdx.x;
     if (o >= sl->live || s >= N) return;
     const SaTry t = sa_try(*sl, sit, o, prm);
@@ -635,14 +638,16 @@ sa_mutate_kernel(const SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ s
     sizes[os] = expf(g[2]) * expf(g[3]);
     float row[9];
     encode_row(g, row);
-    recs[os] = make_rec(preprocess_row(row, H, W, k_sigma));
+    const SplatRec r = make_rec(preprocess_row(row, H, W, k_sigma));
+    recs[os] = r;
+    bnds[os] = rec_bounds(r);
 }
 
 // genetic.py:79-91 on neighbour o: the pick-th later splat bigger than a random
 // splat i trades rows (and raster records) with it
 __global__ void __launch_bounds__(1024)
 sa_swap_kernel(const SaLoopDev* __restrict__ sl, uint32_t k0, uint32_t k1, int N, const float* __restrict__ sizes,
-               float* __restrict__ off, SplatRec* __restrict__ recs) {
+               float* __restrict__ off, SplatRec* __restrict__ recs, int4* __restrict__ bnds) {
     __shared__ int s_scan[16], s_count, s_j;
     const int o = blockIdx.x, tid = threadIdx.x;
     const SaLoopDev& sv = *sl;
@@ -701,17 +706,23 @@ sa_swap_kernel(const SaLoopDev* __restrict__ sl, uint32_t k0, uint32_t k1, int N
         const float4 a = *ri, b = *rj;
         *ri = b;
         *rj = a;
+    } else if (tid == 128) {
+        int4* bi = bnds + (int64_t)o * N + i;
+        int4* bj = bnds + (int64_t)o * N + j;
+        const int4 a = *bi, b = *bj;
+        *bi = b;
+        *bj = a;
     }
 }
 
 hipError_t launch_sa_mutate(hipStream_t st, const SaLoopDev* sl, const SaItDev* sit, const GaParamsDev& prm,
                             uint64_t seed, int N, int cap, const int* tflags, const float* curr, float* off,
-                            float* sizes, SplatRec* recs, int H, int W, float k_sigma) {
+                            float* sizes, SplatRec* recs, int4* bnds, int H, int W, float k_sigma) {
     const int nch = (N + SA_VT - 1) / SA_VT;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     hipLaunchKernelGGL(sa_mutate_kernel, dim3(cap * nch), dim3(SA_VT), 0, st, sl, sit, prm, k0, k1, N, nch, tflags,
-                       curr, off, sizes, recs, H, W, k_sigma);
-    hipLaunchKernelGGL(sa_swap_kernel, dim3(cap), dim3(1024), 0, st, sl, k0, k1, N, sizes, off, recs);
+                       curr, off, sizes, recs, bnds, H, W, k_sigma);
+    hipLaunchKernelGGL(sa_swap_kernel, dim3(cap), dim3(1024), 0, st, sl, k0, k1, N, sizes, off, recs, bnds);
     return hipGetLastError();
 }
 

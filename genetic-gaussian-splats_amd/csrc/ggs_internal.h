@@ -26,11 +26,12 @@ static_assert(sizeof(SplatRec) == 64, "SplatRec must be 64 bytes");
 // live (device, may be null): only the first *live candidates of N splats each are
 // live (the device SA loop sizes its grids for the session's capacity and sets the
 // round's neighbour count on the device); the other threads / waves exit at once.
+// recs [S] and bnds [S] (the records' AABBs, compact for the raster's cull) go together.
 hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_t S, int C, int H,
-                       int W, float k, SplatRec* recs, float* f9, int* i4, float* enc9,
+                       int W, float k, SplatRec* recs, int4* bnds, float* f9, int* i4, float* enc9,
                        const int* live = nullptr, int n_per = 0);
 int raster_tiles(int H, int W, int* nTX);
-hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
+hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty = nullptr,
                          const float* clean = nullptr, const int* live = nullptr);
@@ -140,7 +141,7 @@ hipError_t launch_sa_flags(hipStream_t st, int64_t pos0, int n_tries, int tries,
 // sizes [cap][N] scratch, off [cap][N][9], recs [cap][N].
 hipError_t launch_sa_mutate(hipStream_t st, const SaLoopDev* sl, const SaItDev* sit, const GaParamsDev& prm,
                             uint64_t seed, int N, int cap, const int* tflags, const float* curr, float* off,
-                            float* sizes, SplatRec* recs, int H, int W, float k_sigma);
+                            float* sizes, SplatRec* recs, int4* bnds, int H, int W, float k_sigma);
 // The acceptance uniform of try (it, k): Philox4x32-10 keyed by seed, 53-bit double
 // in [0, 1).  Host and device compute the same bits.
 double sa_accept_uniform(uint64_t seed, uint32_t it, uint32_t k);
@@ -148,7 +149,8 @@ double sa_accept_uniform(uint64_t seed, uint32_t it, uint32_t k);
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
                                float* off, int n_off,    // n_off offspring (GA: P; SA: tries)
-                               SplatRec* recs = nullptr, int H = 0, int W = 0, float k_sigma = 3.0f,
+                               SplatRec* recs = nullptr, int4* bnds = nullptr, int H = 0, int W = 0,
+                               float k_sigma = 3.0f,
                                const SaLoopDev* sl = nullptr, const SaItDev* sit = nullptr);
                                // recs != null: also prep the offspring (records [n_off][N]);
                                // sl != null: SA loop round (neighbour o = try sl->pos + o, its

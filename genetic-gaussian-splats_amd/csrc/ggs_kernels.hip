@@ -47,7 +47,7 @@ using namespace detmath;
 template <bool ENCODE>
 __global__ void __launch_bounds__(256)
 prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, float k,
-            SplatRec* __restrict__ recs, float* __restrict__ f9, int* __restrict__ i4,
+            SplatRec* __restrict__ recs, int4* __restrict__ bnds, float* __restrict__ f9, int* __restrict__ i4,
             float* __restrict__ enc9, const int* __restrict__ live, int n_per) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= S) return;
@@ -65,7 +65,11 @@ prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, f
         for (int j = 0; j < 9; ++j) enc9[i * 9 + j] = row[j];
     }
     const Prep13 p = preprocess_row(row, H, W, k);
-    if (recs) recs[i] = make_rec(p);
+    if (recs) {
+        const SplatRec r = make_rec(p);
+        recs[i] = r;
+        bnds[i] = rec_bounds(r);
+    }
     if (f9) {
         f9[0 * S + i] = p.cx;  f9[1 * S + i] = p.cy;  f9[2 * S + i] = p.sxx;
         f9[3 * S + i] = p.sxy; f9[4 * S + i] = p.syy; f9[5 * S + i] = p.rc;
@@ -201,7 +205,8 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 // partial sum.  TILE_H = 128: 128 accumulator VGPRs (+~35) -> 3 waves per SIMD.
 template <int MODE, bool SAT>
 __global__ void __launch_bounds__(NT, OCC)
-raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int nTX, int nTiles,
+raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, int B, int N, int H, int W, int nTX,
+              int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
@@ -260,13 +265,14 @@ raster_kernel(const SplatRec* __restrict__ recs, int B, int N, int H, int W, int
 #undef GGS_DECL
 
     const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
+    const int4* __restrict__ cbnd = bnds + (int64_t)b * N;
     int* __restrict__ list = &lists[0][0] + wib * CAP;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
 
     // bounds of the next 64 splats are loaded one chunk ahead (the cull does
     // little work per chunk, so it waits on these loads; two chunks ahead: no gain)
-    auto bounds = [&](int i) { return *reinterpret_cast<const int4*>(&crec[max(i, 0)].x0); };
+    auto bounds = [&](int i) { return cbnd[max(i, 0)]; };
     int4 bbn = bounds(N - 1 - lane);
     for (int base = 0; base < N; base += 64) {
         // wave priority: the load-bound cull issues ahead of other waves' blends (+0.4 %)
@@ -698,16 +704,16 @@ hipError_t launch_detmath(hipStream_t st, const float* x, const float* y, int64_
 // launchers (called from ggs_capi.cpp; no allocation, no sync)
 // ---------------------------------------------------------------------------
 hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_t S, int C, int H,
-                       int W, float k, SplatRec* recs, float* f9, int* i4, float* enc9, const int* live,
+                       int W, float k, SplatRec* recs, int4* bnds, float* f9, int* i4, float* enc9, const int* live,
                        int n_per) {
     if (S <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((S + 255) / 256);
     if (encode)
         hipLaunchKernelGGL(prep_kernel<true>, dim3(grid), dim3(256), 0, st, genomes, S, C, H, W, k,
-                           recs, f9, i4, enc9, live, n_per);
+                           recs, bnds, f9, i4, enc9, live, n_per);
     else
         hipLaunchKernelGGL(prep_kernel<false>, dim3(grid), dim3(256), 0, st, genomes, S, C, H, W, k,
-                           recs, f9, i4, enc9, live, n_per);
+                           recs, bnds, f9, i4, enc9, live, n_per);
     return hipGetLastError();
 }
 
@@ -738,7 +744,7 @@ int raster_tiles(int H, int W, int* nTX) {
     return tx * ty;
 }
 
-hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, int N, int H, int W,
+hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty, const float* clean,
                          const int* live) {
@@ -746,7 +752,7 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, int B, 
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
 #define GGS_RASTER(M, S)                                                                       \
-    hipLaunchKernelGGL((raster_kernel<M, S>), grid, block, 0, st, recs, B, N, H, W, nTX, nTiles, \
+    hipLaunchKernelGGL((raster_kernel<M, S>), grid, block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
                        bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live)
     // the saturation check only where strip lists can grow long (N > SAT_MIN_SPLATS);
     // at the bench's 256 splats the kernel without it is the faster code (+1.6 %)

@@ -75,6 +75,11 @@ __device__ __forceinline__ Prep13 preprocess_row(const float g[9], int H, int W,
 
 // Raster coefficients.  exp(-0.5*quad)*a == exp2(e) with
 // e = K*(sxx qx^2 + 2 sxy qx qy + syy qy^2) + log2(a),  K = -0.5*log2(e).
+// The cull's copy of a record's AABB: a compact [B][N] int4 array (16 B per
+// splat; the 64-B records of 1,024-splat candidates overflowed the XCD L2s when
+// every strip-wave's cull walked them, 1024^2 config).
+__device__ __forceinline__ int4 rec_bounds(const SplatRec& r) { return make_int4(r.x0, r.x1, r.y0, r.y1); }
+
 __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
     constexpr float K = -0.72134752044448170f;
     SplatRec r;

@@ -1,0 +1,56 @@
+"""Per-wave timing of one raster launch at any canvas / splat count / batch
+(diagnostic build GGS_TIMING=1), through the host API.
+
+    make -C genetic-gaussian-splats_amd/csrc OUT=../libggs_timing.so BUILD=build_timing EXTRA=-DGGS_TIMING=1
+    GGS_LIB=genetic-gaussian-splats_amd/libggs_timing.so python tools/probe/wave_timing_cfg.py --size 2048 --splats 4096 --batch 1
+
+Prints the launch span, the wave-duration spread, visits per wave, and the grid
+fill: how long at least 3,072 / 2,048 / 1,024 waves were live."""
+import argparse, ctypes as C, json, os, sys
+import numpy as np
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "genetic-gaussian-splats_amd"))
+import ggs
+from ggs import ga
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--size", type=int, default=2048)
+ap.add_argument("--splats", type=int, default=4096)
+ap.add_argument("--batch", type=int, default=1)
+a = ap.parse_args()
+H = W = a.size
+rng = np.random.default_rng(0)
+tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+mask = rng.uniform(0.405, 1, (H, W)).astype(np.float32)
+pop = ga.new_population(a.batch, a.splats, H, W, 3.0, 0.1, np.random.default_rng(a.batch))
+for _ in range(3):
+    ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+n_waves = a.batch * (-(-W // 64)) * (-(-H // 128)) * 4
+buf = np.zeros((n_waves, 8), np.uint64)
+fn = ggs.lib.ggs_debug_timing_read
+fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_size_t]
+assert fn(buf.ctypes.data, buf.nbytes) == 0, "not a GGS_TIMING build?"
+rt0, rt1 = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64)
+t0 = rt0.min()
+s_us, e_us = (rt0 - t0) / 100.0, (rt1 - t0) / 100.0
+dur = e_us - s_us
+visits = buf[:, 6].astype(np.int64)
+ts = np.linspace(0, e_us.max(), 400)
+live = np.array([((s_us <= t) & (e_us > t)).sum() for t in ts])
+dt = ts[1] - ts[0]
+xcc = (buf[:, 5] >> np.uint64(32)).astype(np.int64) & 0xF
+per_xcd_live = np.array([[((s_us <= t) & (e_us > t) & (xcc == x)).sum() for x in range(8)] for t in ts])
+mid = (ts > 0.2 * ts[-1]) & (ts < 0.7 * ts[-1])
+res = {"H": H, "splats": a.splats, "batch": a.batch, "waves": n_waves, "span_us": float(e_us.max()),
+       "wave_us": {k: float(np.percentile(dur, q)) for k, q in (("p10", 10), ("p50", 50), ("p90", 90), ("max", 100))},
+       "wave_us_mean": float(dur.mean()),
+       "visits": {k: int(np.percentile(visits, q)) for k, q in (("p10", 10), ("p50", 50), ("p90", 90), ("max", 100))},
+       "us_with_live_ge": {str(n): float((live >= n).sum() * dt) for n in (3072, 2048, 1024, 512)},
+       "mean_live": float(live.mean()),
+       "last_start_us": float(s_us.max()),
+       "xcd_work_ms": [round(float(dur[xcc == x].sum()) / 1e3, 2) for x in range(8)],
+       "xcd_end_us": [round(float(e_us[xcc == x].max()), 1) for x in range(8)],
+       "xcd_live_mid_mean": [round(float(per_xcd_live[mid, x].mean()), 1) for x in range(8)],
+       "xcd_live_mid_max": [int(per_xcd_live[mid, x].max()) for x in range(8)],
+       "xcd_full_frac_mid": float((per_xcd_live[mid] >= 384).any(axis=1).mean())}
+print(json.dumps(res))
