@@ -290,3 +290,21 @@ def test_device_loop_rejects_mixed_driving():
             sa.propose(0, 2, 0, 2)
     finally:
         sa.close()
+
+
+def test_device_loop_incremental_equals_full_at_configs4_size():
+    """configs[4] size (2048^2, 4,096 splats, 8 tries): the dirty-strip path (only
+    strips a changed splat touches are rasterised, the rest keep the state's
+    partials) gives the full re-render's run bit for bit, at a MUTPB low enough
+    that most strips stay clean."""
+    H = W = 2048
+    target, _, _ = _problem(H, W, 4)
+    init = ga.new_population(1, 4096, H, W, MIN_S, MAX_S, np.random.default_rng(7))[0]
+    kw = dict(mutpb=2e-4, iterations=6, tries_per_iter=8, temp0=1e-3, backend="device", seed=3,
+              init_individual=init)
+    b1, f1, s1 = _sa(target, H, W, 4096, incremental=True, **kw)
+    b0, f0, s0 = _sa(target, H, W, 4096, incremental=False, **kw)
+    np.testing.assert_array_equal(b1, b0)
+    np.testing.assert_array_equal(s1["current"], s0["current"])
+    assert f1 == f0 and s1["curves"] == s0["curves"]
+    assert 0 < s1["stats"]["changed_splats"] < s1["stats"]["proposed"] * 4096 // 4
