@@ -33,6 +33,9 @@ ap.add_argument("--dev-iters", type=int, default=200)
 ap.add_argument("--repeat", type=int, default=3)
 ap.add_argument("--temp0", type=float, default=1e-3)
 ap.add_argument("--only", default="")
+ap.add_argument("--warm", type=int, default=0,
+                help="start from the best state of a --warm-iteration device run (T0 1e-3), so the "
+                     "timed runs see the late-run regime where acceptances are rare")
 a = ap.parse_args()
 H = W = a.size
 target = np.random.default_rng(0).uniform(0, 1, (H, W, 3)).astype(np.float32)
@@ -53,6 +56,11 @@ def evaluate(G):
     return f
 
 
+if a.warm:                       # late-run regime: start from an annealed state
+    init, _ = A.simulated_annealing(
+        target, H, W, "cuda", a.splats, a.mutpb, cfg["mut_sigma_max"], cfg["mut_sigma_min"],
+        "cosine", 3.0, 0.1, 3.0, 0.7, False, a.warm, 1e-3, "cosine", a.tries, seed=9,
+        init_individual=init, progress=False, backend="device")
 res = {}
 variants = (("host_sequential", 1, "host", False, "host"),
             ("host_speculative", None, "host", False, "host"),
@@ -96,4 +104,5 @@ same("host_sequential", "host_speculative")
 same("device_host_loop", "device_loop_full")
 same("device_loop_full", "device_loop_incremental")
 print(json.dumps({"metric": "SA iterations/s", "config": {"H": H, "W": W, "splats": a.splats,
-                  "tries_per_iter": a.tries, "mutpb": a.mutpb, "iters": a.iters}, **res}))
+                  "tries_per_iter": a.tries, "mutpb": a.mutpb, "iters": a.iters, "temp0": a.temp0,
+                  "warm_iters": a.warm}, **res}))
