@@ -322,7 +322,7 @@ int run_fitness(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N,
     if ((rc = ensure(w->bnds, sizeof(int4) * (size_t)std::max<int64_t>(B * N, 1), st))) return rc;
     // one partial per (candidate, tile, 16-column strip)
     if ((rc = ensure(w->partials, sizeof(float) * 4 * (size_t)(B * nTiles), st))) return rc;
-    if ((rc = ensure(w->wpartials, sizeof(float) * 4 * (size_t)nTiles, st))) return rc;
+    if ((rc = ensure(w->wpartials, plan_wsum_bytes(H, W), st))) return rc;
     if ((rc = ensure_tile_order(w, H, W, st))) return rc;
     if (plan_key == 0 || plan_key != w->plan_key) {
         if ((rc = ensure(w->plan, plan_bytes(H, W), st))) return rc;
@@ -540,15 +540,13 @@ int ggs_plan_create(int32_t device, void* stream, const float* d_target_hw3, con
     p->W = W;
     p->mode = mode;
     const hipStream_t st = (hipStream_t)stream;
-    int nTX;
-    const int nTiles = raster_tiles(H, W, &nTX);
     auto bail = [&](int code) {
         if (p->plan.p) (void)hipFree(p->plan.p);
         if (p->wpartials.p) (void)hipFree(p->wpartials.p);
         return code;
     };
     if ((rc = ensure(p->plan, plan_bytes(H, W), st)) ||
-        (rc = ensure(p->wpartials, sizeof(float) * 4 * (size_t)nTiles, st)))
+        (rc = ensure(p->wpartials, plan_wsum_bytes(H, W), st)))
         return bail(rc);
     if (launch_plan(st, d_target_hw3, d_mask_hw, mode, boost_beta, H, W, (float4*)p->plan.p,
                     (float*)p->wpartials.p) != hipSuccess)
@@ -1145,7 +1143,7 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     if ((rc = ensure(s->recs, sizeof(SplatRec) * std::max<size_t>((size_t)s->P * s->N, 1), s->st)) ||
         (rc = ensure(s->bnds, sizeof(int4) * std::max<size_t>((size_t)s->P * s->N, 1), s->st)) ||
         (rc = ensure(s->partials, sizeof(float) * slots * s->P, s->st)) ||
-        (rc = ensure(s->plan, plan_bytes(c.H, c.W), s->st)) || (rc = ensure(s->wpart, sizeof(float) * slots, s->st)) ||
+        (rc = ensure(s->plan, plan_bytes(c.H, c.W), s->st)) || (rc = ensure(s->wpart, plan_wsum_bytes(c.H, c.W), s->st)) ||
         (rc = ensure(s->order, sizeof(int) * (size_t)raster_order_len(c.H, c.W), s->st)))
         return bail(rc);
     std::vector<int> order(raster_order_len(c.H, c.W));
@@ -1293,7 +1291,7 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
         (rc = ensure(s->cur_part, sizeof(float) * slots, s->st)) ||
         (rc = ensure(s->nb_part, sizeof(float) * slots * s->cap, s->st)) ||
         (rc = ensure(s->dirty, slots * s->cap, s->st)) || (rc = ensure(s->plan, plan_bytes(cfg->H, cfg->W), s->st)) ||
-        (rc = ensure(s->wpart, sizeof(float) * slots, s->st)) ||
+        (rc = ensure(s->wpart, plan_wsum_bytes(cfg->H, cfg->W), s->st)) ||
         (rc = ensure(s->order, sizeof(int) * (size_t)raster_order_len(cfg->H, cfg->W), s->st)) ||
         (rc = ensure(s->counters, sizeof(unsigned) * 4, s->st)) || (rc = ensure(s->loop, sizeof(SaLoopDev), s->st)) ||
         (rc = ensure(s->sizes, sizeof(float) * (size_t)std::max(s->N, 1) * s->cap, s->st)))

@@ -41,9 +41,11 @@ hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, cons
                         const SplatRec* nb_recs, int n, int N, int H, int W, unsigned char* dirty,
                         unsigned* n_changed, const int* live = nullptr);
 // Target plan for the fitness epilogue (built once per target/mask/mode/beta).
+// wblock (plan_wsum_bytes): the plan's Sum w as a double, then per-wave sums.
 hipError_t launch_plan(hipStream_t st, const float* target, const float* mask, int mode, float beta,
-                       int H, int W, float4* plan, float* wpartials);
+                       int H, int W, float4* plan, float* wblock);
 size_t plan_bytes(int H, int W);
+size_t plan_wsum_bytes(int H, int W);
 // Tile visiting order for the raster grid: tiles sorted by distance of their
 // centre from the image centre (central tiles carry the most splats; running
 // them first shortens the tail of the launch).

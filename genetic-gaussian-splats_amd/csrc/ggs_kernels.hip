@@ -563,25 +563,32 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 // ---------------------------------------------------------------------------
 // target plan: the fitness epilogue's inputs re-laid out in raster lane order
 // ---------------------------------------------------------------------------
-// One wave per (tile, strip).  For the row-group pair (2k, 2k+1) of the pixel
+// Four waves per (tile, strip), PLAN_KP row-group pairs each (loads unrolled:
+// one wave per strip walking all 16 pairs was a chain of dependent HBM round
+// trips, 23 us at 512^2).  For the row-group pair (2k, 2k+1) of the pixel
 // column this lane owns: plan[((t*4 + strip)*RG + 2k)*64 + lane] =
 // (t_r, t_r', t_g, t_g') and [... + 2k+1] = (t_b, t_b', w, w') (primed: row
 // group 2k+1), the raster epilogue's packed order; w is the pixel weight of
 // fitness.py:17-31 for the mode (1 / mask / 1+beta*clamp(mask)) and 0 outside
-// the image.  wpartials[t*4 + strip] = the strip's sum of w (per-lane in row
-// order, then a lane butterfly).  Target and mask are constant over a GA run,
-// so the plan is built once per (target, mask, mode, beta).
+// the image.  Each wave's sum of w goes to the weight block (plan_wsum_kernel
+// reduces them to the plan's Sum w, a double).  Target and mask are constant
+// over a GA run, so the plan is built once per (target, mask, mode, beta).
+constexpr int PLAN_Q = 4, PLAN_KP = RG / 2 / PLAN_Q;
 __global__ void __launch_bounds__(64)
 plan_kernel(const float* __restrict__ target, const float* __restrict__ mask, int mode, float beta,
-            int H, int W, int nTX, float4* __restrict__ plan, float* __restrict__ wpartials) {
+            int H, int W, int nTX, float4* __restrict__ plan, float* __restrict__ wave_w) {
     const int lane = threadIdx.x;
-    const int t = blockIdx.x >> 2, wv = blockIdx.x & 3;
+    const int sg = blockIdx.x / PLAN_Q, q = blockIdx.x % PLAN_Q;     // strip (t*4 + wv), quarter
+    const int t = sg >> 2, wv = sg & 3;
     const int tx0 = (t % nTX) * TILE, ty0 = (t / nTX) * TILE_H;
     const int col = tx0 + wv * 16 + (lane & 15), ph = lane >> 4;
-    float4* __restrict__ P = plan + (int64_t)blockIdx.x * RG * 64 + lane;
+    float4* __restrict__ P = plan + (int64_t)sg * RG * 64 + lane;
     float wacc = 0.0f;
-    for (int k = 0; k < RG / 2; ++k) {
+#pragma unroll
+    for (int kk = 0; kk < PLAN_KP; ++kk) {
+        const int k = q * PLAN_KP + kk;
         float tr[2], tg[2], tb[2], wg[2];
+#pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int row = ty0 + 4 * (2 * k + h) + ph;
             const bool ok = (row < H) & (col < W);
@@ -599,17 +606,30 @@ plan_kernel(const float* __restrict__ target, const float* __restrict__ mask, in
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wacc += __shfl_xor(wacc, o);
-    if (lane == 0) wpartials[blockIdx.x] = wacc;
+    if (lane == 0) wave_w[blockIdx.x] = wacc;
+}
+
+// Sum w of the plan in float64, fixed order (lane-strided, then the xor
+// butterfly of wave_sum): the weighted / boost modes' denominator
+// (fitness.py:23-31), once per plan instead of once per candidate.
+__global__ void __launch_bounds__(64)
+plan_wsum_kernel(const float* __restrict__ wave_w, int n, double* __restrict__ wsum) {
+    const double v = wave_sum(wave_w, n);
+    if (threadIdx.x == 0) *wsum = v;
 }
 
 hipError_t launch_plan(hipStream_t st, const float* target, const float* mask, int mode, float beta,
-                       int H, int W, float4* plan, float* wpartials) {
+                       int H, int W, float4* plan, float* wblock) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
-    hipLaunchKernelGGL(plan_kernel, dim3(nTiles * 4), dim3(64), 0, st, target, mask, mode, beta, H, W, nTX,
-                       plan, wpartials);
+    const int nw = nTiles * 4 * PLAN_Q;
+    float* wave_w = wblock + 4;                  // after the double (16-B slot)
+    hipLaunchKernelGGL(plan_kernel, dim3(nw), dim3(64), 0, st, target, mask, mode, beta, H, W, nTX, plan, wave_w);
+    hipLaunchKernelGGL(plan_wsum_kernel, dim3(1), dim3(64), 0, st, wave_w, nw, reinterpret_cast<double*>(wblock));
     return hipGetLastError();
 }
+
+size_t plan_wsum_bytes(int H, int W) { return 16 + sizeof(float) * 4 * PLAN_Q * (size_t)raster_tiles(H, W, nullptr); }
 
 // ---------------------------------------------------------------------------
 // dirty strips (incremental SA evaluation, SURVEY.md §8f #4 / annealing.py:121-146)

@@ -133,7 +133,8 @@ __device__ __forceinline__ float finalize_wave(const float* __restrict__ partial
                                                const float* __restrict__ wpartials, int nT, int mode,
                                                double hw, int b) {
     const double num = wave_sum(partials + (int64_t)b * nT, nT);
-    const double wsum = mode != GGS_FIT_NONE ? wave_sum(wpartials, nT) : 0.0;
+    // wpartials: the plan's weight block, Sum w (float64) first (plan_wsum_kernel)
+    const double wsum = mode != GGS_FIT_NONE ? *reinterpret_cast<const double*>(wpartials) : 0.0;
     double v;
     if (mode == GGS_FIT_NONE) v = num / (3.0 * hw);                       // fitness.py:18-19
     else if (mode == GGS_FIT_WEIGHTED) v = num / (wsum + 1e-12);          // fitness.py:28-31
