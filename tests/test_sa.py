@@ -89,3 +89,33 @@ def test_temp_schedules():
         assert all(v > 0 for v in vals) and vals[0] == pytest.approx(1e-3)
         assert all(b <= a for a, b in zip(vals, vals[1:]))
     assert A.temp_schedule("exp", 1.0, 10, 10) == pytest.approx(0.01)
+
+
+def test_device_loop_width_sizes_rounds_to_the_grid():
+    """A device-loop round holds enough neighbours for ~10 rounds of raster wave
+    slots (2048^2: 16 of 2,048 strips; 512^2: 64 of 256), never fewer than one
+    iteration's tries."""
+    assert A.device_loop_width(2048, 2048, 8) == 16
+    assert A.device_loop_width(512, 512, 8) == 64
+    assert A.device_loop_width(4096, 4096, 8) == 8          # 8,192 strips: one iteration's tries
+    assert A.device_loop_width(4096, 4096, 20) == 20
+    assert A.device_loop_width(16, 16, 1) == 64
+
+
+@pytest.mark.parametrize("kw", [dict(loop="device", backend="host"),
+                                dict(loop="bogus", backend="host"),
+                                dict(loop="device", backend="device", draws=object()),
+                                dict(backend="bogus")])
+def test_sa_rejects_inconsistent_loop_arguments(kw):
+    """loop='device' needs the device backend and in-kernel draws; unknown loop /
+    backend names raise before any evaluation."""
+    H = W = 16
+    target = np.random.default_rng(0).uniform(0, 255, (H, W, 3)).astype(np.float32)
+
+    def never(G):                                  # the checks come first
+        raise AssertionError("evaluated")
+    with pytest.raises(ValueError):
+        A.simulated_annealing(target, H, W, "cuda", 4, 0.1, CFG["mut_sigma_max"],
+                              CFG["mut_sigma_min"], "cosine", MIN_S, MAX_S, 3.0, 0.7, False, 2,
+                              1e-3, "cosine", 2, evaluate=never if kw.get("backend") == "host" else None,
+                              progress=False, **kw)
