@@ -69,6 +69,14 @@ def test_input_validation_mirrors_reference_asserts():
     assert rc == -1
     rc = ggs.lib.ggs_fitness_device(0, None, None, 1, 1, 9, None, None, 1, 1.0, 4, 4, 3.0, None)
     assert rc == -1 and b"mask" in ggs.lib.ggs_last_error()
+    # size limits: the raster's cull list holds 32-bit byte offsets of 64-B records
+    # (N * 64 < 2^31), and the grid B * tiles * 4 strips must stay below 2^31
+    rc = ggs.lib.ggs_fitness(None, 1, 2**25, 9, None, None, 0, 1.0, 8, 8, 3.0, None, 0)
+    assert rc == -1 and b"exceeds the limit" in ggs.lib.ggs_last_error()
+    assert ggs.lib.ggs_render(None, 1, 2**25 - 1, 9, 8, 8, 3.0, None, None, 0) != -1 or \
+        b"exceeds" not in ggs.lib.ggs_last_error()
+    rc = ggs.lib.ggs_render(None, 2**30, 1, 9, 1024, 1024, 3.0, None, None, 0)
+    assert rc == -1 and b"grid limit" in ggs.lib.ggs_last_error()
     del C
 
 
