@@ -332,7 +332,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
                 const f2_t e_ = fma2(qyv, fma2((f2_t)s.Cc, qyv, bx2), px2);
                 F2.x = GGS_EXP2(e_.x);
                 F2.y = GGS_EXP2(e_.y);
-                if (__ballot((px > -__builtin_inff()) &
+                if ((__float_as_uint(s.rho4) >> 31) &&          // only flagged splats (make_rec)
+                    __ballot((px > -__builtin_inff()) &
                              (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u))) {
                     GGS_BLEND(0, F2);
                     goto x0;
@@ -341,7 +342,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
                 // d(qy) = 16 Cc (qy + 4) + 8 bx; the .y row's ratio is 2^(64 Cc) times it
                 const float t8_ = px > -__builtin_inff() ? 8.0f * bx : -__builtin_inff();
                 R2.x = GGS_EXP2(__builtin_fmaf(qyv.y, s.c16, t8_));
-                R2.y = R2.x * s.rho4;
+                R2.y = R2.x * __builtin_fabsf(s.rho4);
 #define GGS_FULL(k)                                                                     \
     if ((k) >= 1 && (k) < NPK - 1) {                                                    \
         GGS_BLEND_REC(k)                                                                \
@@ -375,14 +376,15 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             GGS_BLEND(k, fu_);                                                          \
             /* guard on the seed's bits (f >= 0: unsigned order = float order);  */     \
             /* dead lanes (px = -inf) excluded                                    */     \
-            if (__ballot((px > -__builtin_inff()) &                                     \
+            if ((__float_as_uint(s.rho4) >> 31) &&                                      \
+                __ballot((px > -__builtin_inff()) &                                     \
                          (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u))) \
                 goto x##k;                                                              \
             /* live lanes: d <= -e(seed) <= 100; dead lanes: d = -inf -> r = 0;  */     \
             /* d(qy) = 16 Cc (qy + 4) + 8 bx, the .y row's ratio 2^(64 Cc) times */     \
             const float t8_ = px > -__builtin_inff() ? 8.0f * bx : -__builtin_inff();  \
             R2.x = GGS_EXP2(__builtin_fmaf(qy_.y, s.c16, t8_));                         \
-            R2.y = R2.x * s.rho4;                                                       \
+            R2.y = R2.x * __builtin_fabsf(s.rho4);                                      \
             goto u##k;                                                                  \
         }                                                                               \
         break;

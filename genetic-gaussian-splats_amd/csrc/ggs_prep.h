@@ -102,6 +102,23 @@ __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
     r.x1 = p.x1;
     r.y0 = p.y0;
     r.y1 = p.y1;
+    // The raster seeds its row recurrence with the exact value of a visit's first
+    // row pair and walks a thin rotated splat exactly instead when a live seed is
+    // below 2^-100.  Seeds lie in columns [x0, x1] and rows [y0 - 7, y1]; e is
+    // concave along both axes (A, Cc <= 0), so its minimum over that rectangle is
+    // at a corner.  A splat whose corner minimum is at least 2^-99 can never trip
+    // the check: the raster skips it (one margin unit covers the rounding
+    // difference between this and the raster's FMA form of e).  The flag is the
+    // sign bit of rho4 (the raster takes |rho4|): set = run the check.
+    float emin = __builtin_inff();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float qx = (float)((c & 1) ? p.x1 : p.x0) - r.cx;
+        const float qy = (float)((c & 2) ? p.y1 : p.y0 - 7) - r.cy;
+        const float e = qy * (r.Cc * qy + r.Bc * qx) + (r.A * qx * qx + r.la);
+        emin = fminf(emin, e);
+    }
+    if (!(emin >= -99.0f)) r.rho4 = -r.rho4;     // NaN too
     return r;
 }
 
