@@ -354,9 +354,13 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #undef GGS_FULL
                 goto done;
             }
+            // about half the partial visits start at the tile's top (the splat began
+            // in a tile above): test that before the switch's compare tree
+            if (kA == 0) goto f0;
             switch (kA) {
 #define GGS_FIRST(k)                                                                    \
     case k:                                                                             \
+    f##k: __attribute__((unused));                                                      \
         if (k < NPK) {                                                                  \
             const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                  \
             const f2_t e_ = fma2(qy_, fma2((f2_t)s.Cc, qy_, bx2), px2);                        \
