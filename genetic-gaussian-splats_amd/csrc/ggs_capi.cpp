@@ -862,8 +862,11 @@ struct GaSession {
     hipStream_t st = nullptr;
     ggs_ga_config cfg{};
     int P = 0, N = 0, cur = 0, nTiles = 0;
-    DevBuf pop[2], fits[2], off, off_fits, src, target, mask, best_ind, best_fit, best_src,
+    DevBuf pop[2], fits[2], off[2], off_fits, src, target, mask, best_ind, best_fit, best_src,
         best_upd, curves, draws;
+    DevBuf elite[2];               // elite[cur]: rows of pop[cur] by fitness rank (the breed's row map)
+    int ocur = 0;                  // off[ocur]: the offspring evaluated last
+    bool pending = false;          // their survivors / gather not applied yet (ga_flush)
     DevBuf recs, bnds, partials, plan, wpart, order;   // the generation's fused pipeline
     int64_t n_curves = 0, curves_cap = 0;
     void* comm = nullptr;          // ggs_ga_set_comm: offspring fitness sharded over ranks
@@ -953,21 +956,68 @@ int ga_upload_draws(DevBuf& buf, hipStream_t st, int64_t P, int64_t N, int64_t K
     return GGS_OK;
 }
 
+// Survivors + gather of the generation evaluated last (algorithm.py:129-155):
+// population, fitness, best and curves as of the end of that generation.  A
+// generation leaves them pending; the next generation's breed applies them
+// itself (fused), anything reading the session state calls this first.
+int ga_flush(GaSession* s) {
+    if (!s->pending) return GGS_OK;
+    const int P = s->P, N = s->N, nxt = 1 - s->cur;
+    double* row;
+    int rc;
+    if ((rc = ga_curves_row(s, &row))) return rc;
+    // (FitReduce-fused survivors measured slower: 33.7 us vs 19 + 4.1 separately)
+    GGS_HIP(launch_ga_survivors(s->st, (const float*)s->fits[s->cur].p, (const float*)s->off_fits.p, P,
+                                s->cfg.elite_k, (int*)s->src.p, (float*)s->fits[nxt].p, ga_best(s), row, 0,
+                                FitReduce{}, (int*)s->elite[nxt].p));
+    GGS_HIP(launch_ga_gather(s->st, (const float*)s->pop[s->cur].p, (const float*)s->off[s->ocur].p, P, N,
+                             (const int*)s->src.p, (float*)s->pop[nxt].p, ga_best(s), 0));
+    s->cur = nxt;
+    s->n_curves += 1;
+    s->pending = false;
+    return GGS_OK;
+}
+
+// The fused breed (survivors + gather of the previous generation inside the
+// variation kernel: 3 launches per generation instead of 5) up to this population.
+bool ga_fused(const GaSession* s) {
+    static const bool off = getenv("GGS_GA_UNFUSED") && atoi(getenv("GGS_GA_UNFUSED")) != 0;
+    return !off && s->P <= ga_breed_max_population();
+}
+
 int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     GaDrawsDev d{};
     int rc;
     if (hd && (rc = ga_upload_draws(s->draws, s->st, s->P, s->N, s->cfg.tour_k, false, hd, &d))) return rc;
-    const int P = s->P, N = s->N, nxt = 1 - s->cur;
+    const int P = s->P, N = s->N;
     const GaParamsDev prm = ga_params(s->cfg, gen, total);
     const ggs_ga_config& c = s->cfg;
-    // five launches per generation: variation (+ prep of the offspring), raster,
-    // finalize, survivors, gather
-    {   // the offspring's raster records are prepped inside the variation kernel
+    const int onew = 1 - s->ocur;
+    // per generation: breed (survivors + gather of the previous generation, then
+    // variation + prep of the offspring), raster, finalize [, all-gather]
+    if (s->pending && ga_fused(s)) {
+        const int nxt = 1 - s->cur;
+        double* row;
+        if ((rc = ga_curves_row(s, &row))) return rc;
+        BreedDev br{(const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
+                    (const float*)s->off[s->ocur].p, (const float*)s->off_fits.p,
+                    (const int*)s->elite[s->cur].p, (int*)s->elite[nxt].p, (float*)s->pop[nxt].p,
+                    (float*)s->fits[nxt].p, row, ga_best(s), c.elite_k};
+        ProfScope ps(s->st, 0);
+        GGS_HIP(launch_ga_variation(s->st, nullptr, nullptr, P, N, prm, d, c.seed, gen, (float*)s->off[onew].p, P,
+                                    (SplatRec*)s->recs.p, (int4*)s->bnds.p, c.H, c.W, c.k_sigma, nullptr, nullptr,
+                                    &br));
+        s->cur = nxt;
+        s->n_curves += 1;
+    } else {
+        if ((rc = ga_flush(s))) return rc;
         ProfScope ps(s->st, 0);
         GGS_HIP(launch_ga_variation(s->st, (const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
-                                    P, N, prm, d, c.seed, gen, (float*)s->off.p, P, (SplatRec*)s->recs.p,
+                                    P, N, prm, d, c.seed, gen, (float*)s->off[onew].p, P, (SplatRec*)s->recs.p,
                                     (int4*)s->bnds.p, c.H, c.W, c.k_sigma));
     }
+    s->ocur = onew;
+    s->pending = true;
     const float bg[3] = {1.f, 1.f, 1.f};
     // this rank's contiguous shard of the offspring (all of them on one GPU);
     // every rank bred all P offspring above with the same draws
@@ -992,15 +1042,6 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
         if ((rc = ggs_comm_allgather(s->comm, s->st, of + (int64_t)s->rank * per, of, per, 0, nullptr)))
             return rc;
     }
-    double* row;
-    if ((rc = ga_curves_row(s, &row))) return rc;
-    // (FitReduce-fused survivors measured slower: 33.7 us vs 19 + 4.1 separately)
-    GGS_HIP(launch_ga_survivors(s->st, (const float*)s->fits[s->cur].p, (const float*)s->off_fits.p, P,
-                                c.elite_k, (int*)s->src.p, (float*)s->fits[nxt].p, ga_best(s), row, 0));
-    GGS_HIP(launch_ga_gather(s->st, (const float*)s->pop[s->cur].p, (const float*)s->off.p, P, N,
-                             (const int*)s->src.p, (float*)s->pop[nxt].p, ga_best(s), 0));
-    s->cur = nxt;
-    s->n_curves += 1;
     return GGS_OK;
 }
 
@@ -1089,7 +1130,8 @@ void ga_fill_log_bounds(ggs_ga_config* c) {   // utils.py:38-39 when the caller 
 }
 
 void ga_free(GaSession* s) {
-    for (DevBuf* b : {&s->pop[0], &s->pop[1], &s->fits[0], &s->fits[1], &s->off, &s->off_fits, &s->src,
+    for (DevBuf* b : {&s->pop[0], &s->pop[1], &s->fits[0], &s->fits[1], &s->off[0], &s->off[1], &s->off_fits,
+                      &s->src, &s->elite[0], &s->elite[1],
                       &s->target, &s->mask, &s->best_ind, &s->best_fit, &s->best_src, &s->best_upd,
                       &s->curves, &s->draws, &s->recs, &s->bnds, &s->partials, &s->plan, &s->wpart, &s->order})
         if (b->p) (void)hipFree(b->p);
@@ -1126,11 +1168,12 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     auto bail = [&](int code) { ga_free(s.get()); return code; };
     if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(GGS_EHIP, "stream creation failed"));
-    for (DevBuf* b : {&s->pop[0], &s->pop[1], &s->off})
+    for (DevBuf* b : {&s->pop[0], &s->pop[1], &s->off[0], &s->off[1]})
         if ((rc = ensure(*b, std::max<size_t>(pb, 4), s->st))) return bail(rc);
     for (DevBuf* b : {&s->fits[0], &s->fits[1], &s->off_fits})
         if ((rc = ensure(*b, sizeof(float) * s->P, s->st))) return bail(rc);
-    if ((rc = ensure(s->src, sizeof(int) * s->P, s->st))) return bail(rc);
+    for (DevBuf* b : {&s->src, &s->elite[0], &s->elite[1]})
+        if ((rc = ensure(*b, sizeof(int) * s->P, s->st))) return bail(rc);
     if ((rc = ensure(s->target, sizeof(float) * 3 * hw, s->st))) return bail(rc);
     if (mask_hw && (rc = ensure(s->mask, sizeof(float) * hw, s->st))) return bail(rc);
     if ((rc = ensure(s->best_ind, std::max<size_t>(sizeof(float) * 9 * s->N, 4), s->st))) return bail(rc);
@@ -1163,7 +1206,7 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     double* row;
     if ((rc = ga_curves_row(s.get(), &row))) return bail(rc);
     if (launch_ga_survivors(s->st, (const float*)s->fits[0].p, nullptr, s->P, c.elite_k, (int*)s->src.p,
-                            nullptr, ga_best(s.get()), row, 1) ||
+                            nullptr, ga_best(s.get()), row, 1, FitReduce{}, (int*)s->elite[0].p) ||
         launch_ga_gather(s->st, (const float*)s->pop[0].p, nullptr, s->P, s->N, nullptr, nullptr,
                          ga_best(s.get()), 1))
         return bail(fail(GGS_EHIP, "init launch failed"));
@@ -1236,6 +1279,8 @@ int ggs_ga_read(void* handle, float* pop, float* fits, float* best_ind, double* 
     GaSession* s = (GaSession*)handle;
     std::lock_guard<std::mutex> lk(s->c->mu);
     DeviceGuard dg(s->c->dev);
+    const int rc = ga_flush(s);   // the last generation's survivors
+    if (rc) return rc;
     GGS_HIP(hipStreamSynchronize(s->st));
     if (pop) GGS_HIP(hipMemcpy(pop, s->pop[s->cur].p, sizeof(float) * 9 * (size_t)s->P * s->N, hipMemcpyDeviceToHost));
     if (fits) GGS_HIP(hipMemcpy(fits, s->fits[s->cur].p, sizeof(float) * s->P, hipMemcpyDeviceToHost));

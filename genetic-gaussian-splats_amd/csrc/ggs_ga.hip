@@ -190,23 +190,120 @@ __device__ __forceinline__ void mutate_row(float* g, const MaskU& u, const NormD
     for (int c = 5; c < 9; ++c) g[c] = clip(g[c], 0.0f, 255.0f);
 }
 
+// ---------------------------------------------------------------------------
+// breed: survivors + gather of the previous generation fused into the variation
+// ---------------------------------------------------------------------------
+constexpr int ST = 1024;   // max threads; the launch uses min(ST, pow2 >= P) (cheap barriers at P=128)
+constexpr int SMAX = 4096;
+constexpr int RANKMAX = 512;   // counting ranks below this population size (and the fused breed's limit)
+
+// Every breed workgroup rebuilds, in LDS, the next population P_g of
+// algorithm.py:129-141 as a row map: row r < E is the parent of rank r (stable
+// order of the parents' fitness: elite_prev, written by whoever produced that
+// fitness vector — the survivors kernel or the previous breed's stats
+// workgroup, from the same counting rank), row r >= E is offspring r - E of the
+// generation just evaluated.  s_src[r] follows the survivors kernel's index
+// space (parents 0..P-1, offspring P + q), s_nf[r] is the row's fitness.  The
+// rows themselves are read from where they are (no gather in front of the
+// tournament).
+__device__ __forceinline__ int breed_src(const BreedDev& br, int r, int P, int E) {
+    return r < E ? br.elite_prev[r] : P + (r - E);
+}
+__device__ __forceinline__ float breed_fit(const BreedDev& br, int src, int P) {
+    return src < P ? br.fits_prev[src] : br.off_fits[src - P];
+}
+__device__ void breed_rows(const BreedDev& br, int P, float* s_nf, int* s_src) {
+    const int E = br.elite_k < 1 ? 1 : br.elite_k;                      // algorithm.py:129
+    for (int r = threadIdx.x; r < P; r += blockDim.x) {
+        const int src = breed_src(br, r, P, E);
+        s_src[r] = src;
+        s_nf[r] = breed_fit(br, src, P);
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ const float* breed_row(const BreedDev& br, int src, int P, int N) {
+    return src < P ? br.pop_prev + (int64_t)src * N * 9 : br.off_prev + (int64_t)(src - P) * N * 9;
+}
+// The breed grid's extra workgroup: best so far (algorithm.py:143-150), the curves
+// row (:153-155; sequential float64 mean, statistics.median), the best row — the
+// survivors kernel's arithmetic on the same row map, so the same bits — and the
+// next breed's elite list (the median's ranks, rank < E).
+__device__ void breed_stats(const BreedDev& br, int P, int N, const float* s_nf, const int* s_src) {
+    __shared__ float med[2];
+    __shared__ int s_g, s_upd;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int E = br.elite_k < 1 ? 1 : br.elite_k;
+    if (tid == 0) {
+        int g = 0;
+        double sum = (double)s_nf[0];
+        for (int r = 1; r < P; ++r) {
+            if (s_nf[r] < s_nf[g]) g = r;
+            sum += (double)s_nf[r];
+        }
+        const double fg = (double)s_nf[g];
+        const int upd = fg + 1e-10 < *br.best.fit;
+        if (upd) {
+            *br.best.fit = fg;
+            *br.best.src = s_src[g];
+        }
+        *br.best.updated = upd;
+        br.curves_row[0] = *br.best.fit;
+        br.curves_row[1] = sum / (double)P;
+        s_g = g;
+        s_upd = upd;
+    }
+    for (int r = tid; r < P; r += nt) {
+        const float f = s_nf[r];
+        int rank = 0;
+        for (int j = 0; j < P; ++j) rank += (s_nf[j] < f) | ((s_nf[j] == f) & (j < r));
+        if (rank == P / 2) med[1] = f;
+        if (rank == P / 2 - 1) med[0] = f;
+        if (rank < E) br.elite_next[rank] = r;
+    }
+    __syncthreads();
+    if (tid == 0) br.curves_row[2] = (P & 1) ? (double)med[1] : ((double)med[0] + (double)med[1]) / 2.0;
+    if (s_upd) {
+        const float* from = breed_row(br, s_src[s_g], P, N);
+        for (int64_t i = tid; i < (int64_t)N * 9; i += nt) br.best.ind[i] = from[i];
+    }
+}
+
+#ifndef GGS_VTIMING
+#define GGS_VTIMING 0             // diagnostic build: per-workgroup phase clocks (tools/probe/breed_timing.py)
+#endif
+#if GGS_VTIMING
+__device__ unsigned long long g_ggs_vtiming[8 * 4096];
+#define GGS_VMARK(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) \
+    g_ggs_vtiming[8 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define GGS_VMARK(k) do { } while (0)
+#endif
+
 // Threads per variation workgroup (one workgroup per offspring): 256 for a GA
 // generation (P workgroups fill the chip); 1024 when a few large offspring are
 // bred (SA tries at configs[4]: 4,096 splats each), which otherwise leave 16
 // splats per thread on a handful of CUs.  Results do not depend on VT (per-splat
 // work, an OR, a sum and an in-order search).
-template <int VT>
+//
+// BREED: the generation's survivors and gather run inside this kernel (one extra
+// workgroup, o == n_off, keeps best and curves): the parents are the rows of the
+// next population P_g (breed_rows), each workgroup o also writes row o of P_g
+// (and its fitness) for the generation after.  pop / fits are unused then.
+template <int VT, bool BREED>
 __global__ void __launch_bounds__(VT)
 ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fits, int P, int N,
                     GaParamsDev prm, GaDrawsDev d, uint32_t k0, uint32_t k1, int gen,
-                    float* __restrict__ off, SplatRec* __restrict__ recs, int4* __restrict__ bnds, int H, int W,
-                    float k_sigma,
-                    const SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit) {
-    __shared__ int s_a, s_b, s_cx;
+                    float* __restrict__ off, int n_off, SplatRec* __restrict__ recs, int4* __restrict__ bnds,
+                    int H, int W, float k_sigma,
+                    const SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, BreedDev br) {
+    __shared__ int s_a, s_b, s_cx, s_any;
+    __shared__ float s_nf[BREED ? RANKMAX : 1];
+    __shared__ int s_src[BREED ? RANKMAX : 1];
     __shared__ float s_sizei;
     __shared__ int s_j, s_count;
     __shared__ int s_scan[VT / 64];
     const int o = blockIdx.x;                  // offspring index
+    GGS_VMARK(0);
     const int pair = o >> 1;
     const bool first = (o & 1) == 0;
     const int tid = threadIdx.x;
@@ -222,7 +319,225 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
         prm.sig_xy = q.sig[0]; prm.sig_alog = q.sig[1]; prm.sig_blog = q.sig[2];
         prm.sig_theta = q.sig[3]; prm.sig_rgb = q.sig[4]; prm.sig_alpha = q.sig[5];
     }
+    if (BREED && o == n_off) {                 // the stats workgroup
+        breed_rows(br, P, s_nf, s_src);
+        breed_stats(br, P, N, s_nf, s_src);
+        return;
+    }
     const Rng rng{k0, k1, (uint32_t)gen};
+    float* __restrict__ O = off + (int64_t)o * N * 9;
+    const float p = prm.mutpb;
+    const int64_t ob = (int64_t)o * N;
+    const int E = br.elite_k < 1 ? 1 : br.elite_k;
+
+    if (N <= VT) {
+        // One splat per thread (s = tid).  Phase A issues everything that does not
+        // depend on the parents' fitness — the row-map and gather loads (BREED),
+        // the tournament's candidate indices, the crossover decision, every
+        // per-splat draw — with no barrier in between, so the loads' latency
+        // hides behind the Philox / Box-Muller arithmetic; after one barrier
+        // thread 0 only compares fitness values.  The row, its draws and its size
+        // then stay in registers / LDS from mutation to swap to prep.  Same
+        // operations on the same values as the generic path, so the same bits.
+        constexpr int KT = 32;                 // tournament picks precomputed when 2k <= 2*KT
+        __shared__ int s_tour[2 * KT];
+        __shared__ float s_size[VT];
+        __shared__ float s_rowi[9], s_rowj[9];
+        const int sp = tid;
+        const bool act = sp < N;
+        const int k = prm.tour_k;
+        const bool pre = !prm.mutate_only && 2 * k <= 2 * KT;
+        // --- phase A
+        int msrc[(RANKMAX + VT - 1) / VT];               // BREED: row map entries r = tid + VT*i
+        float mfit[(RANKMAX + VT - 1) / VT];
+        float cp[9];                           // BREED: this thread's part of row o of P_g
+        if (BREED) {
+#pragma unroll
+            for (int i = 0; i < (RANKMAX + VT - 1) / VT; ++i) {
+                const int r = tid + VT * i;
+                msrc[i] = r < P ? breed_src(br, r, P, E) : 0;
+                mfit[i] = r < P ? breed_fit(br, msrc[i], P) : 0.0f;
+            }
+            const float* __restrict__ from = breed_row(br, breed_src(br, o, P, E), P, N);
+#pragma unroll
+            for (int c = 0; c < 9; ++c) {
+                const int i = tid + VT * c;
+                cp[c] = i < N * 9 ? from[i] : 0.0f;
+            }
+        }
+        if (tid == 0) {
+            s_any = 0;
+            s_j = -1;
+            if (prm.mutate_only) {
+                s_a = 0;                       // annealing.py:122-128: mutate the current state
+                s_b = 0;
+                s_cx = 0;
+            } else {
+                s_cx = d.cx ? d.cx[pair] : (u01(rng.block(S_CX, (uint32_t)pair, 0).x) < prm.cxpb);
+            }
+        }
+        if (pre && tid < 2 * k) {              // candidate j of parent h's tournament (genetic.py:11)
+            const int h = tid / k, j = tid % k;
+            const int q = h == 0 ? (d.perm ? d.perm[2 * pair] : 2 * pair)
+                                 : (d.perm ? d.perm[(2 * pair + 1) % P] : (2 * pair + 1) % P);
+            s_tour[tid] = d.tour_idx ? d.tour_idx[q * k + j]
+                                     : min((int)(u01(rng.block(S_TOUR, (uint32_t)q, (uint32_t)j).x) * (float)P), P - 1);
+        }
+        MaskU u{};
+        NormD nd{};
+        float cxu = 0.0f;
+        int any = 0;
+        if (act) {
+            u = mask_draws(d, rng, og, ob, sp);
+            any = mask_any(u, p);
+            if (!prm.mutate_only)
+                cxu = d.cx_u ? d.cx_u[(int64_t)pair * N + sp]
+                             : u01(rng.block(S_CX, (uint32_t)pair, (uint32_t)(sp + 1)).x);   // shared by the pair
+            nd = normal_draws(d, rng, og, ob, sp, N);
+        }
+        if (BREED) {
+#pragma unroll
+            for (int i = 0; i < (RANKMAX + VT - 1) / VT; ++i) {
+                const int r = tid + VT * i;
+                if (r < P) {
+                    s_src[r] = msrc[i];
+                    s_nf[r] = mfit[i];
+                }
+            }
+            fits = s_nf;
+        }
+        __syncthreads();
+        GGS_VMARK(1);
+        // --- tournament (genetic.py:8-14, strict <) on the fitness now in place;
+        //     the mask groups' any() (genetic.py:24-29) meanwhile
+        if (tid == 0 && !prm.mutate_only) {
+            if (pre) {
+                int best = -1;
+                for (int j = 0; j < k; ++j) {
+                    const int i = s_tour[j];
+                    if (best < 0 || fits[i] < fits[best]) best = i;
+                }
+                s_a = best;
+                best = -1;
+                for (int j = 0; j < k; ++j) {
+                    const int i = s_tour[k + j];
+                    if (best < 0 || fits[i] < fits[best]) best = i;
+                }
+                s_b = best;
+            } else {
+                const int qa = d.perm ? d.perm[2 * pair] : 2 * pair;
+                const int qb = d.perm ? d.perm[(2 * pair + 1) % P] : (2 * pair + 1) % P;
+                s_a = tournament_pick(fits, d, rng, qa, P, k);
+                s_b = tournament_pick(fits, d, rng, qb, P, k);
+            }
+        }
+        {
+            const int wa = (__ballot(any & ANY_COLOR) ? ANY_COLOR : 0) | (__ballot(any & ANY_XY) ? ANY_XY : 0) |
+                           (__ballot(any & ANY_AB) ? ANY_AB : 0) | (__ballot(any & ANY_T) ? ANY_T : 0);
+            if ((tid & 63) == 0 && wa) atomicOr(&s_any, wa);
+        }
+        __syncthreads();
+        GGS_VMARK(2);
+        any = s_any;
+        const Fallback fb = fallbacks(d, rng, og, o, N, any);
+        const float* __restrict__ A = BREED ? breed_row(br, s_src[s_a], P, N) : pop + (int64_t)s_a * N * 9;
+        const float* __restrict__ Bp = BREED ? breed_row(br, s_src[s_b], P, N) : pop + (int64_t)s_b * N * 9;
+        GGS_VMARK(3);
+        float g[9];
+        if (act) {
+            // genetic.py:17-21 (c1 = where(m, a, b), c2 = where(m, b, a)) / duplicate
+            const bool m = cxu < 0.5f;
+            const bool takeA = s_cx ? (first ? m : !m) : first;
+            const float* src = (takeA ? A : Bp) + (int64_t)sp * 9;
+#pragma unroll
+            for (int c = 0; c < 9; ++c) g[c] = src[c];
+            mutate_row(g, u, nd, fb, sp, prm);
+            s_size[sp] = expf(g[2]) * expf(g[3]);
+        }
+        if (N >= 2) {
+            // genetic.py:79-91: pick i, then the pick-th later splat bigger than i
+            const int i = d.swap_i ? d.swap_i[o] : (int)(rng.block(S_IND, og, 4).x % (uint32_t)(N - 1));
+            __syncthreads();
+            GGS_VMARK(4);
+            const float sizei = s_size[i];
+            const bool c = act && sp > i && s_size[sp] > sizei;
+            const uint64_t bal = __ballot(c);
+            const int lane = tid & 63, w = tid >> 6;
+            if (lane == 0) s_scan[w] = __popcll(bal);
+            __syncthreads();
+            int count = 0, before = 0;
+            for (int q = 0; q < VT / 64; ++q) {
+                before += q < w ? s_scan[q] : 0;
+                count += s_scan[q];
+            }
+            if (count > 0) {
+                int pick;
+                if (d.swap_pick && d.swap_pick[o] >= 0) pick = d.swap_pick[o];
+                else {
+                    const double uu = d.swap_u ? d.swap_u[o] : (double)u01(rng.block(S_IND, og, 5).x);
+                    pick = (int)(uu * (double)count);
+                    if (pick > count - 1) pick = count - 1;
+                }
+                const int inwave = __popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+                if (c && before + inwave == pick) s_j = sp;       // the (pick+1)-th in splat order
+                __syncthreads();
+                const int j = s_j;
+                if (sp == i) {
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) s_rowi[q] = g[q];
+                }
+                if (sp == j) {
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) s_rowj[q] = g[q];
+                }
+                __syncthreads();
+                if (sp == i) {
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) g[q] = s_rowj[q];
+                }
+                if (sp == j) {
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) g[q] = s_rowi[q];
+                }
+            }
+        }
+        GGS_VMARK(5);
+        if (act) {
+#pragma unroll
+            for (int c = 0; c < 9; ++c) O[(int64_t)sp * 9 + c] = g[c];
+            if (recs) {         // prep fused in (ggs_prep.h): the raster's record of this splat
+                float row[9];
+                encode_row(g, row);
+                const SplatRec r = make_rec(preprocess_row(row, H, W, k_sigma));
+                recs[ob + sp] = r;
+                bnds[ob + sp] = rec_bounds(r);
+            }
+        }
+        if (BREED) {            // gather: row o of P_g and its fitness, for the generation after
+            float* __restrict__ to = br.pop_next + (int64_t)o * N * 9;
+#pragma unroll
+            for (int c = 0; c < 9; ++c) {
+                const int i = tid + VT * c;
+                if (i < N * 9) to[i] = cp[c];
+            }
+            if (tid == 0) br.fits_next[o] = s_nf[o];
+        }
+#if GGS_VTIMING
+        __syncthreads();
+#endif
+        GGS_VMARK(6);
+        return;
+    }
+
+    // ---- generic path (N > VT: several splats per thread) ------------------------
+    if (BREED) {
+        breed_rows(br, P, s_nf, s_src);
+        const float* __restrict__ from = breed_row(br, s_src[o], P, N);     // gather: row o of P_g
+        float* __restrict__ to = br.pop_next + (int64_t)o * N * 9;
+        for (int64_t i = tid; i < (int64_t)N * 9; i += VT) to[i] = from[i];
+        if (tid == 0) br.fits_next[o] = s_nf[o];
+        fits = s_nf;
+    }
     if (tid == 0 && prm.mutate_only) {
         s_a = 0;                               // annealing.py:122-128: mutate the current state
         s_b = 0;
@@ -237,11 +552,8 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
         else s_cx = u01(rng.block(S_CX, (uint32_t)pair, 0).x) < prm.cxpb;
     }
     __syncthreads();
-    const float* __restrict__ A = pop + (int64_t)s_a * N * 9;
-    const float* __restrict__ Bp = pop + (int64_t)s_b * N * 9;
-    float* __restrict__ O = off + (int64_t)o * N * 9;
-    const float p = prm.mutpb;
-    const int64_t ob = (int64_t)o * N;
+    const float* __restrict__ A = BREED ? breed_row(br, s_src[s_a], P, N) : pop + (int64_t)s_a * N * 9;
+    const float* __restrict__ Bp = BREED ? breed_row(br, s_src[s_b], P, N) : pop + (int64_t)s_b * N * 9;
 
     // pass 1: crossover + mask flags, any() per mask group
     int any = 0;
@@ -352,9 +664,6 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
 // ---------------------------------------------------------------------------
 // survivors: elites by stable fitness order, next fitness vector, best, curves
 // ---------------------------------------------------------------------------
-constexpr int ST = 1024;   // max threads; the launch uses min(ST, pow2 >= P) (cheap barriers at P=128)
-constexpr int SMAX = 4096;
-constexpr int RANKMAX = 512;   // counting ranks below this population size
 
 // bitonic sort of n2 (power of two) LDS keys (+ optional indices), ascending;
 // ties by index: lexicographic (key, idx) == Python's stable sorted()
@@ -381,7 +690,8 @@ __device__ void bitonic(float* key, int* idx, int n2) {
 __global__ void __launch_bounds__(ST)
 ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ off_fits, int P,
                     int elite_k, int* __restrict__ src, float* __restrict__ new_fits,
-                    GaBestDev best, double* __restrict__ curves_row, int init, FitReduce fr) {
+                    GaBestDev best, double* __restrict__ curves_row, int init, FitReduce fr,
+                    int* __restrict__ elite_next) {
     // The surviving offspring's fitness (rows E..P-1 of the next generation):
     // given, or reduced here from the raster's strip partials, one wave per
     // candidate (finalize_wave: the same bits as finalize_kernel).
@@ -456,6 +766,7 @@ ga_survivors_kernel(const float* __restrict__ fits, const float* __restrict__ of
             for (int j = 0; j < P; ++j) rank += (nf[j] < f) | ((nf[j] == f) & (j < r));
             if (rank == P / 2) med[1] = f;
             if (rank == P / 2 - 1) med[0] = f;
+            if (elite_next && rank < E) elite_next[rank] = r;    // the fused breed's row map
         }
         __syncthreads();
         if (tid == 0)
@@ -526,23 +837,29 @@ ga_gather_kernel(const float* __restrict__ pop, const float* __restrict__ off, i
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
                                float* off, int n_off, SplatRec* recs, int4* bnds, int H, int W, float k_sigma,
-                               const SaLoopDev* sl, const SaItDev* sit) {
-    if (n_off < 64 && N >= 1024)
-        hipLaunchKernelGGL(ga_variation_kernel<1024>, dim3(n_off), dim3(1024), 0, st, pop, fits, P, N, prm, d,
-                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, bnds, H, W, k_sigma, sl, sit);
-    else
-        hipLaunchKernelGGL(ga_variation_kernel<256>, dim3(n_off), dim3(256), 0, st, pop, fits, P, N, prm, d,
-                           (uint32_t)seed, (uint32_t)(seed >> 32), gen, off, recs, bnds, H, W, k_sigma, sl, sit);
+                               const SaLoopDev* sl, const SaItDev* sit, const BreedDev* br) {
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    if (br) {       // + the stats workgroup
+        if (P > RANKMAX || n_off != P) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((ga_variation_kernel<256, true>), dim3(n_off + 1), dim3(256), 0, st, pop, fits, P, N,
+                           prm, d, k0, k1, gen, off, n_off, recs, bnds, H, W, k_sigma, sl, sit, *br);
+    } else if (n_off < 64 && N >= 1024) {
+        hipLaunchKernelGGL((ga_variation_kernel<1024, false>), dim3(n_off), dim3(1024), 0, st, pop, fits, P, N,
+                           prm, d, k0, k1, gen, off, n_off, recs, bnds, H, W, k_sigma, sl, sit, BreedDev{});
+    } else {
+        hipLaunchKernelGGL((ga_variation_kernel<256, false>), dim3(n_off), dim3(256), 0, st, pop, fits, P, N,
+                           prm, d, k0, k1, gen, off, n_off, recs, bnds, H, W, k_sigma, sl, sit, BreedDev{});
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_ga_survivors(hipStream_t st, const float* fits, const float* off_fits, int P,
                                int elite_k, int* src, float* new_fits, const GaBestDev& best,
-                               double* curves_row, int init, const FitReduce& fr) {
+                               double* curves_row, int init, const FitReduce& fr, int* elite_next) {
     int nt = fr.partials ? 512 : 64;   // 8 waves for the fused per-candidate reductions
     while (nt < P && nt < ST) nt <<= 1;
     hipLaunchKernelGGL(ga_survivors_kernel, dim3(1), dim3(nt), 0, st, fits, off_fits, P, elite_k,
-                       src, new_fits, best, curves_row, init, fr);
+                       src, new_fits, best, curves_row, init, fr, elite_next);
     return hipGetLastError();
 }
 
@@ -554,6 +871,12 @@ hipError_t launch_ga_gather(hipStream_t st, const float* pop, const float* off, 
 }
 
 int ga_max_population() { return SMAX; }
+#if GGS_VTIMING
+extern "C" int ggs_debug_vtiming_read(void* host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ggs_vtiming), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+#endif
+int ga_breed_max_population() { return RANKMAX; }
 
 // ---------------------------------------------------------------------------
 // device SA loop (ggs_sa_run): chunk start, and one round's acceptance walk

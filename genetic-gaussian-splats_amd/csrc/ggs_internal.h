@@ -148,12 +148,26 @@ hipError_t launch_sa_mutate(hipStream_t st, const SaLoopDev* sl, const SaItDev* 
 // in [0, 1).  Host and device compute the same bits.
 double sa_accept_uniform(uint64_t seed, uint32_t it, uint32_t k);
 
+struct BreedDev {               // the fused breed (launch_ga_variation with br != null)
+    const float* pop_prev;      // [P][N][9] population P_{g-1} (materialised)
+    const float* fits_prev;     // [P] its fitness
+    const float* off_prev;      // [P][N][9] offspring of generation g-1
+    const float* off_fits;      // [P] their fitness (finalize / all-gather)
+    const int* elite_prev;      // [E] rows of P_{g-1} by rank (survivors / the previous breed)
+    int* elite_next;            // [E] the same for P_g (written by the stats workgroup)
+    float* pop_next;            // [P][N][9] P_g, row o written by workgroup o
+    float* fits_next;           // [P]
+    double* curves_row;         // [3] best, mean, median of P_g
+    GaBestDev best;
+    int elite_k;
+};
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,
                                float* off, int n_off,    // n_off offspring (GA: P; SA: tries)
                                SplatRec* recs = nullptr, int4* bnds = nullptr, int H = 0, int W = 0,
                                float k_sigma = 3.0f,
-                               const SaLoopDev* sl = nullptr, const SaItDev* sit = nullptr);
+                               const SaLoopDev* sl = nullptr, const SaItDev* sit = nullptr,
+                               const BreedDev* br = nullptr);
                                // recs != null: also prep the offspring (records [n_off][N]);
                                // sl != null: SA loop round (neighbour o = try sl->pos + o, its
                                // iteration's sigmas from sit; o >= sl->live exits)
@@ -165,10 +179,12 @@ struct FitReduce {               // survivors reduces the offspring's strip part
 };
 hipError_t launch_ga_survivors(hipStream_t st, const float* fits, const float* off_fits, int P,
                                int elite_k, int* src, float* new_fits, const GaBestDev& best,
-                               double* curves_row, int init, const FitReduce& fr = FitReduce{});
+                               double* curves_row, int init, const FitReduce& fr = FitReduce{},
+                               int* elite_next = nullptr);   // P <= 512: rows of the output by rank, rank < E
 hipError_t launch_ga_gather(hipStream_t st, const float* pop, const float* off, int P, int N,
                             const int* src, float* next, const GaBestDev& best, int init);
 int ga_max_population();
+int ga_breed_max_population();   // the fused breed's population limit
 
 // ---- RCCL (ggs_comm.cpp) ----------------------------------------------------
 // Grouped in-place all-gather over single-process communicators (ggs_comm_init_local):

@@ -130,6 +130,10 @@ void ggs_plan_destroy(void* plan);
  * genetic_approx's generation loop (algorithm.py:85-155) on one device: the
  * population, fitness, elites, best individual and curves stay in HBM; a
  * generation is variation -> fitness -> survivors -> gather, no host sync.
+ * Up to pop_size 512 the survivors/gather of a generation run inside the next
+ * generation's variation launch ("breed": 3 launches per generation instead of
+ * 5); ggs_ga_read applies the last generation's first, so what it returns is the
+ * same either way (GGS_GA_UNFUSED=1 in the environment: always 5 launches).
  * Draws: explicit arrays (ggs_ga_step with draws != NULL; replay / parity) or a
  * counter-based Philox4x32-10 stream keyed by (seed, generation, individual). */
 typedef struct ggs_ga_config {

@@ -44,8 +44,9 @@ def _problem(H, W, seed):
     (24, 24, 6, 1, 3, 2, 0, 0.5, 0.5, False, 4),       # N = 1: no swap; elite_k 0 -> 1
     (16, 16, 600, 3, 2, 3, 25, 0.5, 0.1, False, 5),    # P > 512: bitonic survivors path
 ])
+@pytest.mark.parametrize("chunk", [2, 8])   # 8 >= G: one run, every later generation a fused breed
 def test_device_ga_matches_host_ga_with_same_draws(H, W, P, N, G, tour_k, elite_k, cxpb, mutpb,
-                                                    boost, seed):
+                                                    boost, seed, chunk):
     target, t, m = _problem(H, W, seed)
     init = ga.new_population(P, N, H, W, MIN_S, MAX_S, np.random.default_rng(seed))
     rec = RecordingDraws(ga.NumpyDraws(seed), cxpb)
@@ -55,7 +56,7 @@ def test_device_ga_matches_host_ga_with_same_draws(H, W, P, N, G, tour_k, elite_
               return_state=True, **CFG)
     hb, hf, hs = ga.genetic_approx(target, H, W, "cuda", draws=rec, **kw)
     assert len(rec.generations) == G
-    db, df, ds = ga.genetic_approx(target, H, W, "cuda", draws=rec, backend="device", chunk=2, **kw)
+    db, df, ds = ga.genetic_approx(target, H, W, "cuda", draws=rec, backend="device", chunk=chunk, **kw)
     np.testing.assert_array_equal(ds["population"], hs["population"])
     np.testing.assert_array_equal(ds["fitness"], hs["fitness"])
     np.testing.assert_array_equal(db, hb)
@@ -133,6 +134,47 @@ def test_device_ga_philox_run():
     assert f2 == f1
     _, _, s3 = ga.genetic_approx(target, H, W, "cuda", seed=12, chunk=30, **kw)
     assert not np.array_equal(s3["population"], s1["population"])
+
+
+_FUSED_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from ggs import ga
+from ggs.ga_device import DeviceGA
+from ggs.mask import compute_importance_mask, prepare_target
+H = W = 512
+target = np.random.default_rng(0).uniform(0, 255, (H, W, 3)).astype(np.float32)
+t = prepare_target(target, H, W)
+m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
+init = ga.new_population(128, 256, H, W, 3.0, 0.1, np.random.default_rng(0))
+cfg = dict(mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0, "alpha": 25.0},
+           mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0, "alpha": 2.0},
+           schedule="cosine")
+dga = DeviceGA(t, m, init, tour_k=2, elite_k=8, cxpb=0.05, mutpb=0.05, min_scale_splats=3.0,
+               max_scale_splats=0.1, seed=1, **cfg)
+dga.run(1, 25, 25)
+st = dga.read()
+np.savez(sys.argv[2], population=st["population"], fitness=st["fitness"], best=st["best"],
+         best_fit=st["best_fit"], **{"c_" + k: np.asarray(v) for k, v in st["curves"].items()})
+"""
+
+
+def test_device_ga_fused_breed_equals_unfused(tmp_path):
+    """The fused breed (survivors + gather inside the variation kernel) against the
+    five-launch generation (GGS_GA_UNFUSED=1) at the bench workload, 25 generations
+    of Philox draws in one run: identical populations, fitness, best and curves."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.dirname(os.path.dirname(ggs.__file__))
+    out = {}
+    for tag, env in (("fused", {}), ("unfused", {"GGS_GA_UNFUSED": "1"})):
+        path = str(tmp_path / f"{tag}.npz")
+        subprocess.run([sys.executable, "-c", _FUSED_SCRIPT, pkg, path], check=True, timeout=300,
+                       env=dict(os.environ, **env))
+        out[tag] = np.load(path)
+    for k in out["fused"].files:
+        np.testing.assert_array_equal(out["fused"][k], out["unfused"][k], err_msg=k)
 
 
 def test_device_ga_rejects_bad_config():
