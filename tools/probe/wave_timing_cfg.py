@@ -47,6 +47,9 @@ res = {"H": H, "splats": a.splats, "batch": a.batch, "waves": n_waves, "span_us"
        "visits": {k: int(np.percentile(visits, q)) for k, q in (("p10", 10), ("p50", 50), ("p90", 90), ("max", 100))},
        "us_with_live_ge": {str(n): float((live >= n).sum() * dt) for n in (3072, 2048, 1024, 512)},
        "mean_live": float(live.mean()),
+       "phase_frac": {k: round(float(buf[:, i].astype(np.float64).sum() / buf[:, 2:5].astype(np.float64).sum()), 3)
+                      for k, i in (("cull", 2), ("visits", 3), ("epilogue", 4))},
+       "clk_per_visit_p50": float(np.median(buf[:, 3].astype(np.float64) / np.maximum(visits, 1))),
        "last_start_us": float(s_us.max()),
        "xcd_work_ms": [round(float(dur[xcc == x].sum()) / 1e3, 2) for x in range(8)],
        "xcd_end_us": [round(float(e_us[xcc == x].max()), 1) for x in range(8)],
