@@ -121,7 +121,7 @@ __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirst
 #if GGS_TIMING
 constexpr int GGS_TIMING_WAVES = 1 << 16;
 // per wave (blockIdx, WPB = 1): realtime start, realtime end (100 MHz), cull,
-// visit and epilogue shader clocks, HW_ID | XCC_ID << 24, visits, unused
+// visit and epilogue shader clocks, HW_ID | XCC_ID << 24, listed visits, blended visits
 __device__ unsigned long long g_ggs_timing[8 * GGS_TIMING_WAVES];
 #define GGS_TMARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
@@ -217,7 +217,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #if GGS_TIMING
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_cull = 0, t_vis = 0, t_mark = __builtin_amdgcn_s_memtime();
-    unsigned n_vis = 0;
+    unsigned n_vis = 0, n_done = 0;     // listed / blended visits
 #endif
     const int wib = ufirst((int)(threadIdx.x >> 6));  // wave in block (uniform: keeps control on SALU)
     // SA loop rounds: the grid is sized for the session's capacity and only the
@@ -304,6 +304,9 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         int offv = list[min(lane, cnt - 1)];
         // one (splat, strip) visit: cull-list record s -> the strip's accumulators
         auto visit = [&](const SplatRec& s) __attribute__((always_inline)) {
+#if GGS_TIMING
+            ++n_done;
+#endif
             const int x0 = s.x0, x1 = s.x1, y0 = s.y0, y1 = s.y1;
             const int dy0 = y0 - ty0, dy1 = y1 - ty0;          // AABB rows relative to the tile
             const int gA = max(dy0, 0) >> 2;                   // first / last row group
@@ -560,7 +563,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             o[0] = rt_start; o[1] = rt_end; o[2] = t_cull; o[3] = t_vis; o[4] = now - t_mark;
             o[5] = (unsigned long long)__builtin_amdgcn_s_getreg(0xF804) |
                    ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);
-            o[6] = n_vis; o[7] = 0;
+            o[6] = n_vis; o[7] = n_done;
         }
     }
 #endif

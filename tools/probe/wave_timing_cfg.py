@@ -49,7 +49,10 @@ res = {"H": H, "splats": a.splats, "batch": a.batch, "waves": n_waves, "span_us"
        "mean_live": float(live.mean()),
        "phase_frac": {k: round(float(buf[:, i].astype(np.float64).sum() / buf[:, 2:5].astype(np.float64).sum()), 3)
                       for k, i in (("cull", 2), ("visits", 3), ("epilogue", 4))},
-       "clk_per_visit_p50": float(np.median(buf[:, 3].astype(np.float64) / np.maximum(visits, 1))),
+       "blended": {k: int(np.percentile(buf[:, 7].astype(np.int64), q)) for k, q in (("p50", 50), ("max", 100))},
+       "clk_per_blended_visit_p50": float(np.median(buf[:, 3].astype(np.float64) /
+                                                    np.maximum(buf[:, 7].astype(np.float64), 1))),
+       "ns_per_blended_visit_p50": float(np.median(dur * 1e3 / np.maximum(buf[:, 7].astype(np.float64), 1))),
        "last_start_us": float(s_us.max()),
        "xcd_work_ms": [round(float(dur[xcc == x].sum()) / 1e3, 2) for x in range(8)],
        "xcd_end_us": [round(float(e_us[xcc == x].max()), 1) for x in range(8)],
