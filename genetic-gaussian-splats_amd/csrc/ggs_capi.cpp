@@ -596,6 +596,80 @@ int ggs_render_device(int32_t device, void* stream, const float* d_genomes, int6
     return run_render(c, (hipStream_t)stream, d_genomes, B, N, C, H, W, k_sigma, bg ? bg : bg1, d_out_bhw3);
 }
 
+}  // extern "C"
+
+namespace ggs {
+namespace {
+uint64_t host_plan_key(uint64_t tkey, uint64_t mkey, float boost_beta, int mode, int H, int W) {
+    uint32_t bb;
+    memcpy(&bb, &boost_beta, 4);
+    return (((tkey * 0x9E3779B97F4A7C15ull) ^ (mkey + 0x632BE59BD9B4E019ull) ^ ((uint64_t)bb << 8) ^
+             ((uint64_t)mode << 2) ^ ((uint64_t)H << 40) ^ ((uint64_t)W << 20)) & ~(1ull << 63)) | 1;
+}
+
+// One device, host arrays in and out.  The content hashes of target and mask
+// (4 MB at 512^2: ~0.2 ms on one core) decide whether the device copies cached
+// from an earlier call are still right.  A GA passes the same arrays every
+// generation, so the evaluation is enqueued against the cached copies first and
+// the arrays are hashed while the GPU runs; only if the contents changed is the
+// result discarded and the evaluation redone with the new inputs (same bits as
+// hashing first).  *done = 0: nothing cached yet, the caller takes the plain path.
+int fitness_one_device_speculative(DevCtx* c, const float* genomes_axes, int64_t B, int N, int C,
+                                   const float* target_hw3, const float* mask_hw, int mode, float boost_beta,
+                                   int H, int W, float k_sigma, float* out_B, int* done) {
+    *done = 0;
+    const size_t tbytes = sizeof(float) * 3 * (size_t)H * W, mbytes = sizeof(float) * (size_t)H * W;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->target_key == 0 || c->target_bytes != tbytes || !c->target.p ||
+        (mask_hw && (c->mask_key == 0 || c->mask_bytes != mbytes || !c->mask.p)))
+        return GGS_OK;
+    DeviceGuard dg(c->dev);
+    hipStream_t st = c->stream;
+    const size_t gbytes = sizeof(float) * (size_t)N * C * (size_t)B;
+    int rc;
+    if ((rc = ensure(c->out, sizeof(float) * (size_t)B, st))) return rc;
+    if ((rc = ensure_pinned(c->h_out, sizeof(float) * (size_t)B))) return rc;
+    if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
+    if ((rc = ensure_pinned(c->h_gen, std::max<size_t>(gbytes, 4)))) return rc;
+    GGS_HIP(hipStreamSynchronize(st));  // pinned staging may still feed a previous copy
+    if (gbytes) {
+        memcpy(c->h_gen.p, genomes_axes, gbytes);
+        GGS_HIP(hipMemcpyAsync(c->gen.p, c->h_gen.p, gbytes, hipMemcpyHostToDevice, st));
+    }
+    const uint64_t mkey_c = mask_hw ? c->mask_key : 0;
+    auto evaluate = [&](uint64_t tk, uint64_t mk) {
+        int r = run_fitness(c, st, (const float*)c->gen.p, B, N, C, (const float*)c->target.p,
+                            mask_hw ? (const float*)c->mask.p : nullptr, mode, boost_beta, H, W, k_sigma,
+                            (float*)c->out.p, host_plan_key(tk, mk, boost_beta, mode, H, W));
+        if (r) return r;
+        GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, sizeof(float) * (size_t)B, hipMemcpyDeviceToHost, st));
+        return GGS_OK;
+    };
+    if ((rc = evaluate(c->target_key, mkey_c))) return rc;
+    const uint64_t tkey = hash_bytes(target_hw3, tbytes);      // while the GPU runs
+    const uint64_t mkey = mask_hw ? hash_bytes(mask_hw, mbytes) : 0;
+    GGS_HIP(hipStreamSynchronize(st));
+    if (tkey != c->target_key || mkey != mkey_c) {            // changed: redo with the new inputs
+        if (tkey != c->target_key) {
+            GGS_HIP(hipMemcpyAsync(c->target.p, target_hw3, tbytes, hipMemcpyHostToDevice, st));
+            c->target_key = tkey;
+        }
+        if (mask_hw && mkey != c->mask_key) {
+            GGS_HIP(hipMemcpyAsync(c->mask.p, mask_hw, mbytes, hipMemcpyHostToDevice, st));
+            c->mask_key = mkey;
+        }
+        if ((rc = evaluate(tkey, mkey))) return rc;
+        GGS_HIP(hipStreamSynchronize(st));
+    }
+    memcpy(out_B, c->h_out.p, sizeof(float) * (size_t)B);
+    *done = 1;
+    return GGS_OK;
+}
+}  // namespace
+}  // namespace ggs
+
+extern "C" {
+
 int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, const float* target_hw3,
                 const float* mask_hw, int32_t mode, float boost_beta, int32_t H, int32_t W,
                 float k_sigma, float* out_B, int32_t n_devices) {
@@ -609,13 +683,19 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
     if ((rc = active_ctxs(n_devices, &cs))) return rc;
     const int nd = (int)cs.size();
     const size_t tbytes = sizeof(float) * 3 * (size_t)H * W, mbytes = sizeof(float) * (size_t)H * W;
-    const uint64_t tkey = hash_bytes(target_hw3, tbytes);
-    const uint64_t mkey = mask_hw ? hash_bytes(mask_hw, mbytes) : 0;
     const size_t row = (size_t)N * C;
-    const int64_t per = (B + nd - 1) / nd;
     // RCCL gather of the shards (GGS_FANOUT_RCCL=1 forces it at one device: tests)
     static const bool force_rccl = getenv("GGS_FANOUT_RCCL") && atoi(getenv("GGS_FANOUT_RCCL")) != 0;
     const bool gather = nd > 1 || force_rccl;
+    if (!gather) {
+        int done = 0;
+        if ((rc = fitness_one_device_speculative(cs[0], genomes_axes, B, N, C, target_hw3, mask_hw, mode,
+                                                 boost_beta, H, W, k_sigma, out_B, &done)) || done)
+            return rc;
+    }
+    const uint64_t tkey = hash_bytes(target_hw3, tbytes);
+    const uint64_t mkey = mask_hw ? hash_bytes(mask_hw, mbytes) : 0;
+    const int64_t per = (B + nd - 1) / nd;
 
     std::vector<std::unique_lock<std::mutex>> locks;
     for (int d = 0; d < nd; ++d) locks.emplace_back(cs[d]->mu);
@@ -653,14 +733,10 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
             memcpy(c->h_gen.p, genomes_axes + row * b0, gbytes);
             GGS_HIP(hipMemcpyAsync(c->gen.p, c->h_gen.p, gbytes, hipMemcpyHostToDevice, st));
         }
-        uint32_t bb;
-        memcpy(&bb, &boost_beta, 4);
-        const uint64_t pkey = ((tkey * 0x9E3779B97F4A7C15ull) ^ (mkey + 0x632BE59BD9B4E019ull) ^
-                               ((uint64_t)bb << 8) ^ ((uint64_t)mode << 2) ^ ((uint64_t)H << 40) ^
-                               ((uint64_t)W << 20)) & ~(1ull << 63);
         if ((rc = run_fitness(c, st, (const float*)c->gen.p, nb, N, C, (const float*)c->target.p,
                               mask_hw ? (const float*)c->mask.p : nullptr, mode, boost_beta, H, W,
-                              k_sigma, (float*)c->out.p + (gather ? b0 : 0), pkey | 1)))
+                              k_sigma, (float*)c->out.p + (gather ? b0 : 0),
+                              host_plan_key(tkey, mkey, boost_beta, mode, H, W))))
             return rc;
         if (!gather)
             GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, sizeof(float) * nb, hipMemcpyDeviceToHost, st));

@@ -344,6 +344,48 @@ def test_target_cache_sees_content_change(full_size):
     np.testing.assert_array_equal(ggs.fitness(pop[:4], tgt, H, W, 3.0, weight_mask=mask), a)
 
 
+def test_target_cache_speculation_in_place_and_mode_changes(full_size):
+    """The host API evaluates against the cached target/mask while it hashes the
+    caller's arrays (ggs_capi.cpp fitness_one_device_speculative): every result
+    must equal a fresh evaluation of the arrays as they are at the call — after
+    in-place edits of the same buffers, a mask-only change, a mode change and a
+    switch to no mask."""
+    pop, tgt, mask, H, W = full_size
+    P = pop[:8]
+    t, m = tgt.copy(), mask.copy()
+
+    from ggs import hip
+
+    def fresh(t_, m_, boost_only=False):         # device-pointer API: no host-side target cache
+        st = hip.Stream()
+        g, td, out = hip.DeviceArray.from_host(P), hip.DeviceArray.from_host(t_), hip.DeviceArray((len(P),))
+        md = hip.DeviceArray.from_host(m_) if m_ is not None else None
+        mode = ggs.GGS_FIT_NONE if m_ is None else (ggs.GGS_FIT_BOOST if boost_only else ggs.GGS_FIT_WEIGHTED)
+        plan = ggs.TargetPlan(0, st.handle, td.ptr, md.ptr if md is not None else 0, mode, 1.0, H, W)
+        plan.fitness_device(st.handle, g.ptr, len(P), P.shape[1], 9, 3.0, out.ptr)
+        st.synchronize()
+        r = out.to_host()
+        plan.close()
+        return r
+
+    a = ggs.fitness(P, t, H, W, 3.0, weight_mask=m)
+    np.testing.assert_array_equal(ggs.fitness(P, t, H, W, 3.0, weight_mask=m), a)   # speculation hit
+    t[10:300, 50:90] = 0.25                                                           # target edited in place
+    b = ggs.fitness(P, t, H, W, 3.0, weight_mask=m)
+    assert (a != b).all()
+    np.testing.assert_array_equal(b, fresh(t, m))
+    m[:, :256] = 1.0                                                                  # mask edited in place
+    c = ggs.fitness(P, t, H, W, 3.0, weight_mask=m)
+    assert (c != b).any()
+    np.testing.assert_array_equal(c, fresh(t, m))
+    d = ggs.fitness(P, t, H, W, 3.0, weight_mask=m, boost_only=True)                  # mode change
+    np.testing.assert_array_equal(d, fresh(t, m, boost_only=True))
+    np.testing.assert_array_equal(a, ggs.fitness(P, tgt, H, W, 3.0, weight_mask=mask))   # back again
+    e = ggs.fitness(P, t, H, W, 3.0)                                                  # no mask
+    np.testing.assert_array_equal(e, fresh(t, None))
+    np.testing.assert_array_equal(ggs.fitness(P, t, H, W, 3.0, weight_mask=m), c)
+
+
 def test_full_size_two_streams_concurrent_bit_identical(full_size):
     """bench.py's schedule: batches alternate over two HIP streams (one workspace
     each) with both in flight at once; every batch's fitness has the same bits as
