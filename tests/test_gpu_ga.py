@@ -177,6 +177,33 @@ def test_device_ga_fused_breed_equals_unfused(tmp_path):
         np.testing.assert_array_equal(out["fused"][k], out["unfused"][k], err_msg=k)
 
 
+def test_device_ga_read_is_idempotent_and_resumable():
+    """ggs_ga_read applies a pending generation's survivors once: reading twice
+    returns the same state and curve count, and stepping on after a read gives the
+    same run as never reading (fused breeds across the read boundary)."""
+    H = W = 48
+    P, N = 24, 40
+    _, t, m = _problem(H, W, 3)
+    init = ga.new_population(P, N, H, W, MIN_S, MAX_S, np.random.default_rng(3))
+    kw = dict(tour_k=2, elite_k=3, cxpb=0.4, mutpb=0.1, min_scale_splats=MIN_S, max_scale_splats=MAX_S,
+              seed=5, **CFG)
+    a, b = DeviceGA(t, m, init, **kw), DeviceGA(t, m, init, **kw)
+    try:
+        a.run(1, 6, 12)
+        r1, r2 = a.read(), a.read()
+        np.testing.assert_array_equal(r1["population"], r2["population"])
+        assert r1["curves"] == r2["curves"] and len(r1["curves"]["best"]) == 7
+        a.run(7, 6, 12)
+        b.run(1, 12, 12)
+        ra, rb = a.read(), b.read()
+        for k in ("population", "fitness", "best"):
+            np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
+        assert ra["best_fit"] == rb["best_fit"] and ra["curves"] == rb["curves"]
+    finally:
+        a.close()
+        b.close()
+
+
 def test_device_ga_rejects_bad_config():
     H = W = 16
     _, t, m = _problem(H, W, 0)
