@@ -62,10 +62,15 @@ struct Rng {
     }
 };
 
-__device__ __forceinline__ float normal_from(uint32_t a, uint32_t b) {   // Box-Muller
+// Box-Muller pair from two Philox words: r = sqrt(-2 ln u1) with u1 in (0, 1],
+// angle 2*pi*u2.  The hardware transcendentals (v_log_f32 = log2, v_sqrt_f32,
+// v_sin/v_cos_f32 in revolutions) are ample for mutation noise and keep the
+// per-splat draw chain short; both outputs are used (5 pairs cover a splat's 9).
+__device__ __forceinline__ float2 normal_pair(uint32_t a, uint32_t b) {
     const float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);      // (0, 1]
-    const float u2 = u01(b);
-    return sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
+    const float u2 = u01(b);                                               // [0, 1) revolutions
+    const float r = __builtin_amdgcn_sqrtf(-1.38629436112f * __builtin_amdgcn_logf(u1));   // -2 ln 2 * log2
+    return make_float2(r * __builtin_amdgcn_cosf(u2), r * __builtin_amdgcn_sinf(u2));
 }
 
 // ---------------------------------------------------------------------------
@@ -153,13 +158,11 @@ __device__ __forceinline__ NormD normal_draws(const GaDrawsDev& d, const Rng& rn
         const U4 g1 = rng.block(S_NORM_A, og, (uint32_t)s);
         const U4 g2 = rng.block(S_NORM_B, og, (uint32_t)s);
         const U4 g3 = rng.block(S_NORM_C, og, (uint32_t)s);
-        n.nx0 = normal_from(g1.x, g1.y); n.nx1 = normal_from(g1.z, g1.w);
-        n.na0 = normal_from(g2.x, g2.y); n.na1 = normal_from(g2.z, g2.w);
-        n.nt = normal_from(g3.x, g3.y); n.nr0 = normal_from(g3.z, g3.w);
-        const U4 g4 = rng.block(S_NORM_C, og, (uint32_t)(s + N));
-        n.nr1 = normal_from(g4.x, g4.y); n.nr2 = normal_from(g4.z, g4.w);
-        const U4 g5 = rng.block(S_NORM_C, og, (uint32_t)(s + 2 * N));
-        n.nr3 = normal_from(g5.x, g5.y);
+        const float2 p1 = normal_pair(g1.x, g1.y), p2 = normal_pair(g1.z, g1.w);
+        const float2 p3 = normal_pair(g2.x, g2.y), p4 = normal_pair(g2.z, g2.w);
+        const float2 p5 = normal_pair(g3.x, g3.y);
+        n.nx0 = p1.x; n.nx1 = p1.y; n.na0 = p2.x; n.na1 = p2.y;
+        n.nt = p3.x; n.nr0 = p3.y; n.nr1 = p4.x; n.nr2 = p4.y; n.nr3 = p5.x;
     }
     return n;
 }

@@ -91,6 +91,9 @@ for name, spec, backend, inc, loop in variants:
                  "setup_ms": round(t_setup * 1e3, 1), "accepted": st["stats"].get("accepted"),
                  "eval_ms_per_iter": round(ev["s"] / a.iters * 1e3, 2) if backend == "host" else None,
                  "launches": st["stats"]["launches"], "evaluated": st["stats"]["evaluated"],
+                 # trajectory-independent rates (the it/s of one seed depend on its acceptances)
+                 "us_per_round": round(dt * 1e6 / max(1, st["stats"]["launches"]), 1),
+                 "us_per_evaluated": round(dt * 1e6 / max(1, st["stats"]["evaluated"]), 1),
                  "changed_splats_per_neighbour": round(st["stats"]["changed_splats"] /
                                                        max(1, st["stats"]["proposed"]), 1)
                  if "changed_splats" in st["stats"] else None,
