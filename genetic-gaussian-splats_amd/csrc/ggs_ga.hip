@@ -970,11 +970,18 @@ sa_mutate_kernel(const SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ s
 }
 
 // genetic.py:79-91 on neighbour o: the pick-th later splat bigger than a random
-// splat i trades rows (and raster records) with it
-__global__ void __launch_bounds__(1024)
+// splat i trades rows (and raster records) with it.  Thread t owns the contiguous
+// run of splats [t*per, (t+1)*per) (splat order = thread order), counts its
+// candidates in one read of the sizes, one workgroup scan of the counts gives the
+// total (-> pick) and each run's rank offset, and the thread whose run holds the
+// pick walks its run again to name j.  Two barriers (the first version counted,
+// then walked the sizes in 1024-splat chunks with three barriers per chunk: 8.4 us
+// per round at 4,096 splats).
+constexpr int SW_THREADS = 1024;
+__global__ void __launch_bounds__(SW_THREADS)
 sa_swap_kernel(const SaLoopDev* __restrict__ sl, uint32_t k0, uint32_t k1, int N, const float* __restrict__ sizes,
                float* __restrict__ off, SplatRec* __restrict__ recs, int4* __restrict__ bnds) {
-    __shared__ int s_scan[16], s_count, s_j;
+    __shared__ int s_wsum[SW_THREADS / 64], s_j;
     const int o = blockIdx.x, tid = threadIdx.x;
     const SaLoopDev& sv = *sl;
     if (o >= sv.live || N < 2) return;
@@ -984,43 +991,40 @@ sa_swap_kernel(const SaLoopDev* __restrict__ sl, uint32_t k0, uint32_t k1, int N
     const float* __restrict__ sz = sizes + (int64_t)o * N;
     const int i = (int)(rng.block(S_IND, og, 4).x % (uint32_t)(N - 1));
     const float sizei = sz[i];
-    const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+    const int lane = tid & 63, w = tid >> 6;
+    const int per = (N + SW_THREADS - 1) / SW_THREADS;
+    const int r0 = min(tid * per, N), r1 = min(r0 + per, N);
     int cnt = 0;
-    for (int s = tid; s < N; s += blockDim.x) cnt += (s > i) && (sz[s] > sizei);
-    for (int k = 32; k > 0; k >>= 1) cnt += __shfl_xor(cnt, k);
-    if (lane == 0) s_scan[w] = cnt;
+    for (int sk = max(r0, i + 1); sk < r1; ++sk) cnt += sz[sk] > sizei;
+    int v = cnt;                                       // inclusive wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(v, d);
+        if (lane >= d) v += u;
+    }
+    if (lane == 63) s_wsum[w] = v;
     if (tid == 0) s_j = -1;
     __syncthreads();
-    if (tid == 0) {
-        int tot = 0;
-        for (int k = 0; k < nw; ++k) tot += s_scan[k];
-        s_count = tot;
+    int before = v - cnt, count = 0;
+#pragma unroll
+    for (int q = 0; q < SW_THREADS / 64; ++q) {
+        const int t = s_wsum[q];
+        before += q < w ? t : 0;
+        count += t;
     }
-    __syncthreads();
-    const int count = s_count;
-    if (count == 0) return;
+    if (count == 0) return;                            // (uniform)
     int pick = (int)((double)u01(rng.block(S_IND, og, 5).x) * (double)count);
     if (pick > count - 1) pick = count - 1;
-    int seen = 0;
-    for (int base = 0; base < N; base += blockDim.x) {   // the (pick+1)-th candidate in splat order
-        const int s = base + tid;
-        const bool c = s < N && s > i && sz[s] > sizei;
-        const uint64_t bal = __ballot(c);
-        const int inwave = __popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
-        __syncthreads();
-        if (lane == 0) s_scan[w] = __popcll(bal);
-        __syncthreads();
-        int before = seen;
-        for (int k = 0; k < w; ++k) before += s_scan[k];
-        if (c && before + inwave == pick) s_j = s;
-        int tot = 0;
-        for (int k = 0; k < nw; ++k) tot += s_scan[k];
-        seen += tot;
-        __syncthreads();
-        if (s_j >= 0) break;
+    if (pick >= before && pick < before + cnt) {       // this run holds the (pick+1)-th candidate
+        int left = pick - before;
+        for (int sk = max(r0, i + 1); sk < r1; ++sk)
+            if (sz[sk] > sizei && left-- == 0) {
+                s_j = sk;
+                break;
+            }
     }
+    __syncthreads();
     const int j = s_j;
-    if (j < 0) return;
     float* __restrict__ O = off + (int64_t)o * N * 9;
     if (tid < 9) {
         const float a = O[(int64_t)i * 9 + tid], b = O[(int64_t)j * 9 + tid];
@@ -1048,7 +1052,7 @@ hipError_t launch_sa_mutate(hipStream_t st, const SaLoopDev* sl, const SaItDev* 
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     hipLaunchKernelGGL(sa_mutate_kernel, dim3(cap * nch), dim3(SA_VT), 0, st, sl, sit, prm, k0, k1, N, nch, tflags,
                        curr, off, sizes, recs, bnds, H, W, k_sigma);
-    hipLaunchKernelGGL(sa_swap_kernel, dim3(cap), dim3(1024), 0, st, sl, k0, k1, N, sizes, off, recs, bnds);
+    hipLaunchKernelGGL(sa_swap_kernel, dim3(cap), dim3(SW_THREADS), 0, st, sl, k0, k1, N, sizes, off, recs, bnds);
     return hipGetLastError();
 }
 
@@ -1139,12 +1143,15 @@ sa_accept_kernel(SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, Sa
     float* __restrict__ best = r.best;
     // install: 16-B copies (the genome is 36 N bytes: N % 4 floats of tail)
     const int64_t n9 = (int64_t)N * 9, n4 = n9 >> 2;
-    const float* src = r.nb + j * n9;
-    const float4* s4 = reinterpret_cast<const float4*>(src);
-    float4* c4 = reinterpret_cast<float4*>(curr);
-    float4* b4 = reinterpret_cast<float4*>(best);
+    const float* __restrict__ src = r.nb + j * n9;
+    const float4* __restrict__ s4 = reinterpret_cast<const float4*>(src);
+    float4* __restrict__ c4 = reinterpret_cast<float4*>(curr);
+    float4* __restrict__ b4 = reinterpret_cast<float4*>(best);
     const bool nbst = s_nb;
     if (((j * n9) & 3) == 0) {
+        // distinct buffers (restrict): the unrolled loads go out together instead of
+        // one load-store round trip per iteration
+#pragma unroll 8
         for (int64_t i = threadIdx.x; i < n4; i += blockDim.x) {
             const float4 v = s4[i];
             c4[i] = v;
