@@ -313,31 +313,41 @@ def save_curves_csv(curves: Dict[str, Sequence[float]], out_csv_path: str) -> No
 def save_loss_curve_png(curves, out_path: str, title: str = "GA fitness over generations",
                         xlabel: str = "Generation", ylabel: str = "MSE", log_y: bool = False,
                         dpi: int = 144) -> None:
-    """utils.py:85-130 (matplotlib, when installed; otherwise a warning as there)."""
+    """utils.py:85-130: one line per named curve against its index, written as a
+    PNG.  Same contract as the reference: nothing when out_path is empty; a
+    warning and no file without matplotlib or without any values; ValueError when
+    the non-empty curves differ in length."""
     if not out_path:
         return
     try:
         import matplotlib
         matplotlib.use("Agg")
-        import matplotlib.pyplot as plt
-    except Exception as e:  # noqa: BLE001 — mirrors the reference's fallback
+        from matplotlib.figure import Figure
+    except Exception as e:  # noqa: BLE001 — the reference degrades to a warning too
         print(f"[warn] matplotlib not available, cannot save plot: {e}")
         return
     os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)
-    plt.figure()
-    for name, values in curves.items():
-        if len(values):
-            plt.plot(range(len(values)), values, label=name)
-    plt.title(title)
-    plt.xlabel(xlabel)
-    plt.ylabel(ylabel)
+    series = {k: list(v) for k, v in curves.items() if len(v)}
+    if not series:
+        print("[warn] No values to plot")
+        return
+    lengths = {k: len(v) for k, v in series.items()}
+    n = next(iter(lengths.values()))
+    bad = [k for k, m in lengths.items() if m != n]
+    if bad:
+        raise ValueError(f"Curve '{bad[0]}' length {lengths[bad[0]]} does not match others {n}")
+    fig = Figure()
+    ax = fig.add_subplot()
+    x = np.arange(n)
+    for name, ys in series.items():
+        ax.plot(x, ys, label=name)
+    ax.set(title=title, xlabel=xlabel, ylabel=ylabel)
     if log_y:
-        plt.yscale("log")
-    plt.grid(True, which="both", alpha=0.3)
-    plt.legend()
-    plt.tight_layout()
-    plt.savefig(out_path, dpi=dpi)
-    plt.close()
+        ax.set_yscale("log")
+    ax.grid(True, which="both", alpha=0.3)
+    ax.legend()
+    fig.tight_layout()
+    fig.savefig(out_path, dpi=dpi)
 
 
 def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_splats: int,

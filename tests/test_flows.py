@@ -34,6 +34,22 @@ def test_resize_helpers_match_reference_semantics():
     assert out is not g
 
 
+def test_loss_curve_png_contract(tmp_path, capsys):
+    """utils.py:85-130's contract: a PNG per call, nothing for an empty path, a
+    warning (no file) without values, ValueError for curves of unequal length."""
+    pytest.importorskip("matplotlib")
+    from ggs.ga import save_loss_curve_png
+    out = tmp_path / "sub" / "loss.png"
+    save_loss_curve_png({"best": [3.0, 2.0, 1.0], "mean": [4.0, 3.0, 2.5], "empty": []}, str(out), log_y=True)
+    assert out.read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"
+    save_loss_curve_png({"best": [1.0]}, "")                       # no path: nothing
+    none = tmp_path / "none.png"
+    save_loss_curve_png({"best": []}, str(none))
+    assert not none.exists() and "No values to plot" in capsys.readouterr().out
+    with pytest.raises(ValueError):
+        save_loss_curve_png({"a": [1.0, 2.0], "b": [1.0]}, str(tmp_path / "bad.png"))
+
+
 def test_per_individual_operator_drop_ins():
     from modules import genetic, population, utils
     population.seed(1)
