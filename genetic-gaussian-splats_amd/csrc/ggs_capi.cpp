@@ -1599,12 +1599,16 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
     // Rounds are enqueued in batches with one host sync between batches: a round
     // consumes at most its width in tries, so ceil(remaining / width) rounds never
     // overshoot the chunk (rounds past its end would be empty launches anyway).
+    // A batch holds at most GGS_SA_MAX_ROUNDS_PER_SYNC rounds (ggs_sa_rounds_per_sync):
+    // unbounded, a 256-iteration chunk at high acceptance queued ~1,000 rounds =
+    // 4,000 dispatches behind one sync, and rocprofv3's PMC dispatch interception
+    // crashed the host thread inside the launch call.
     const uint64_t evaluated0 = s->h_loop->evaluated;
     int64_t remaining = end - pos0;
     int est = width > 0 ? width : (s->h_loop->acc_rate < 1.0 / s->cap ? s->cap
                                    : std::max(1, (int)lrint(1.0 / s->h_loop->acc_rate)));
     for (;;) {
-        const int64_t R = std::max<int64_t>(1, (remaining + est - 1) / std::max(1, est));
+        const int64_t R = ggs_sa_rounds_per_sync(remaining, est);
         for (int64_t r = 0; r < R; ++r)
             if ((rc = round())) return rc;
         GGS_HIP(hipMemcpyAsync(s->h_loop, loop, sizeof(SaLoopDev), hipMemcpyDeviceToHost, s->st));
@@ -1644,10 +1648,27 @@ int ggs_sa_accept_uniform(uint64_t seed, int32_t it, int32_t k, double* u) {
     return GGS_OK;
 }
 
+int64_t ggs_sa_rounds_per_sync(int64_t remaining, int32_t est) {
+    const int64_t e = std::max<int64_t>(1, est);
+    const int64_t R = std::max<int64_t>(1, (std::max<int64_t>(remaining, 0) + e - 1) / e);
+    return std::min<int64_t>(R, GGS_SA_MAX_ROUNDS_PER_SYNC);
+}
+
 int ggs_sa_set_incremental(void* handle, int32_t on) {
     if (!handle) return fail(GGS_EINVAL, "null handle");
     SaSession* s = (SaSession*)handle;
     std::lock_guard<std::mutex> lk(s->c->mu);
+    if (on && !s->incremental) {
+        // The device loop installs an accepted neighbour's records and strip
+        // partials only while incremental evaluation is on (sa_accept_kernel), so
+        // after an incremental-off ggs_sa_run they describe an older state:
+        // re-evaluate the current state before the dirty-strip test relies on them.
+        DeviceGuard dg(s->c->dev);
+        int rc = sa_eval(s, (const float*)s->curr.p, 1, (SplatRec*)s->cur_recs.p, (int4*)s->nb_bnds.p,
+                         (float*)s->cur_part.p, (float*)s->nb_fits.p, false);
+        if (rc) return rc;
+        GGS_HIP(hipStreamSynchronize(s->st));
+    }
     s->incremental = on != 0;
     return GGS_OK;
 }

@@ -86,6 +86,7 @@ SIGNATURES = {
     "ggs_sa_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ggs_sa_run": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                              C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_double)]),
+    "ggs_sa_rounds_per_sync": (C.c_int64, [C.c_int64, C.c_int32]),
     "ggs_sa_loop_state": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                     C.POINTER(C.c_uint64)]),
@@ -198,13 +199,24 @@ def check(rc: int, what: str) -> None:
     raise GGSError(f"{msg} (code {rc})")
 
 
+# The C library's device list (ggs_select_devices) is process-wide state: the
+# host API selects its call's devices and makes the call under this lock, and
+# ``selected`` mirrors what was last handed to the library by anyone.
+device_lock = threading.RLock()
+selected = [None]
+
+
 def select_devices(ids) -> int:
     """Restrict the host API to these HIP device ids (empty: all)."""
     ensure_init()
+    ids = tuple(int(i) for i in ids)
     arr = (C.c_int32 * max(len(ids), 1))(*ids)
-    rc = lib.ggs_select_devices(arr, len(ids))
-    if rc < 0:
-        check(rc, "ggs_select_devices")
+    with device_lock:
+        selected[0] = None                    # unknown until the call succeeds
+        rc = lib.ggs_select_devices(arr, len(ids))
+        if rc < 0:
+            check(rc, "ggs_select_devices")
+        selected[0] = ids
     return rc
 
 

@@ -7,9 +7,9 @@ unchanged.  Every compute call goes through ctypes into libggs.so.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
-import threading
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -62,15 +62,15 @@ def device_index(device=None) -> int:
     return int(idx)
 
 
-_selected = [None]                  # the device list last handed to ggs_select_devices
-_sel_lock = threading.Lock()
-
-
-def _use_devices(device, n_devices: int) -> int:
-    """Point the host API at the devices of one call and return the n_devices
-    argument for the C layer.  n_devices == 1 (default): the single device
-    ``device`` names; n_devices > 1: fan the batch out over the first n_devices
-    GPUs (opt-in; one RCCL gather returns the scalars); n_devices <= 0: all GPUs."""
+@contextlib.contextmanager
+def _on_devices(device, n_devices: int):
+    """Point the host API at the devices of one call and yield the n_devices
+    argument for the C layer; the selection and the call happen under one lock
+    (another thread, or a direct ``ggs.select_devices``, cannot change the
+    library's device list in between).  n_devices == 1 (default): the single
+    device ``device`` names; n_devices > 1: fan the batch out over the first
+    n_devices GPUs (opt-in; one RCCL gather returns the scalars); n_devices <= 0:
+    all GPUs."""
     n = _lib.ensure_init()
     if n_devices == 1:
         ids = (device_index(device),)
@@ -78,11 +78,10 @@ def _use_devices(device, n_devices: int) -> int:
             raise _lib.GGSDeviceError(f"device {device!r} -> HIP device {ids[0]}, but {n} visible")
     else:
         ids = tuple(range(n if n_devices <= 0 else min(int(n_devices), n)))
-    with _sel_lock:
-        if _selected[0] != ids:
+    with _lib.device_lock:
+        if _lib.selected[0] != ids:
             _lib.select_devices(list(ids))
-            _selected[0] = ids
-    return len(ids)
+        yield len(ids)
 
 
 def render(genomes, H: int, W: int, *, k_sigma: float = 3.0,
@@ -98,13 +97,13 @@ def render(genomes, H: int, W: int, *, k_sigma: float = 3.0,
     g = _genomes3d(genomes, "render")
     B, N, Cc = g.shape
     H, W = int(H), int(W)
-    nd = _use_devices(device, n_devices)
     out = np.empty((B, H, W, 3), np.float32)
     bg = np.ascontiguousarray(np.broadcast_to(np.asarray(background, np.float32), (3,)))
     if fp16_canvas:
         bg = bg.astype(np.float16).astype(np.float32)
-    check(lib.ggs_render(_fp(g), B, N, Cc, H, W, float(k_sigma), _fp(bg), _fp(out), nd),
-          "ggs_render")
+    with _on_devices(device, n_devices) as nd:
+        check(lib.ggs_render(_fp(g), B, N, Cc, H, W, float(k_sigma), _fp(bg), _fp(out), nd),
+              "ggs_render")
     if fp16_canvas:
         out = out.astype(np.float16).astype(np.float32)
     return out
@@ -115,7 +114,7 @@ def fitness(genomes_axes, target, H: int, W: int, k_sigma: float = 3.0,
             device=None, n_devices: int = 1) -> np.ndarray:
     """fitness.py:7-31 on a stacked [B,N,C] axes-angle batch → float32 [B]
     (on the GPU ``device`` names; ``n_devices`` > 1 opts into the multi-GPU
-    fan-out, see ``_use_devices``)."""
+    fan-out, see ``_on_devices``)."""
     g = _genomes3d(genomes_axes, "fitness")
     B, N, Cc = g.shape
     H, W = int(H), int(W)
@@ -130,10 +129,10 @@ def fitness(genomes_axes, target, H: int, W: int, k_sigma: float = 3.0,
             raise GGSInputError(f"weight_mask must be [H,W] = {(H, W)}, got {tuple(mask.shape)}")
         mode = _lib.GGS_FIT_BOOST if boost_only else _lib.GGS_FIT_WEIGHTED
         mask_p = _fp(mask)
-    nd = _use_devices(device, n_devices)
     out = np.empty((B,), np.float32)
-    check(lib.ggs_fitness(_fp(g), B, N, Cc, _fp(tgt), mask_p, mode, float(boost_beta), H, W,
-                          float(k_sigma), _fp(out), nd), "ggs_fitness")
+    with _on_devices(device, n_devices) as nd:
+        check(lib.ggs_fitness(_fp(g), B, N, Cc, _fp(tgt), mask_p, mode, float(boost_beta), H, W,
+                              float(k_sigma), _fp(out), nd), "ggs_fitness")
     return out
 
 
@@ -147,8 +146,8 @@ def encode(G_axes) -> np.ndarray:
     lead = g.shape[:-1]
     flat = np.ascontiguousarray(g.reshape(-1, g.shape[-1]))
     out = np.empty((flat.shape[0], 9), np.float32)
-    _use_devices(None, 1)
-    check(lib.ggs_encode(_fp(flat), flat.shape[0], flat.shape[1], _fp(out)), "ggs_encode")
+    with _on_devices(None, 1):
+        check(lib.ggs_encode(_fp(flat), flat.shape[0], flat.shape[1], _fp(out)), "ggs_encode")
     return out.reshape(*lead, 9)
 
 
@@ -161,9 +160,9 @@ def preprocess(genome, H: int, W: int, k_sigma: float = 3.0) -> Dict[str, np.nda
     S = g.shape[0]
     f9 = np.empty((9, S), np.float32)
     i4 = np.empty((4, S), np.int32)
-    _use_devices(None, 1)
-    check(lib.ggs_preprocess(_fp(g), S, g.shape[1], int(H), int(W), float(k_sigma), _fp(f9),
-                             i4.ctypes.data_as(_i32p)), "ggs_preprocess")
+    with _on_devices(None, 1):
+        check(lib.ggs_preprocess(_fp(g), S, g.shape[1], int(H), int(W), float(k_sigma), _fp(f9),
+                                 i4.ctypes.data_as(_i32p)), "ggs_preprocess")
     keys = ("cx", "cy", "sxx", "sxy", "syy", "rc", "gc", "bc", "a")
     out = {k: f9[i] for i, k in enumerate(keys)}
     out.update({k: i4[i] for i, k in enumerate(("x0", "x1", "y0", "y1"))})

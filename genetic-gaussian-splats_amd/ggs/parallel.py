@@ -8,13 +8,14 @@ exchange — and the only collective is one all-gather of the shards' float32
 fitness scalars per generation over RCCL (xGMI), issued by libggs itself
 (``ggs_comm_*``).  No PyTorch on this path: the 128-byte RCCL id travels
 through a file rendezvous on the node (``file_rendezvous``).  ``ShardedFitness``
-and ``gather_shards`` keep a ``torch.distributed`` transport for callers that
-already run a process group (the CPU tests use ``gloo``).
+gathers through an ``RcclGather`` by default and keeps a ``torch.distributed``
+transport (``gather_shards``) for callers that already run a process group.
 """
 from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 import tempfile
 import time
 from typing import Callable, Optional, Tuple
@@ -47,30 +48,42 @@ def gather_shards(local: np.ndarray, B: int, group=None, device=None) -> np.ndar
 
 
 class ShardedFitness:
-    """fitness_population over every rank of a process group.
+    """fitness_population (fitness.py:34-47) over every rank of a job.
 
     Each rank holds the same population (e.g. a GA driven with the same seed on
-    every rank, or broadcast by rank 0), evaluates its shard on its local GPU
-    through libggs.so and receives the full fitness vector.
+    every rank, or broadcast by rank 0), evaluates its contiguous shard on its
+    local GPU through libggs.so and receives the full fitness vector.
+
+    Transport, in this order: ``comm`` (an :class:`RcclGather`, or any object
+    with ``rank``, ``world`` and ``allgather_host``); a ``torch.distributed``
+    ``group`` (or the default group when one is initialised); otherwise an
+    :class:`RcclGather` made here from the launcher's environment — the
+    torch-free path (RCCL id through ``file_rendezvous``).
 
     ``evaluate(G_shard) -> [b]`` defaults to :func:`ggs.fitness` with the target
-    and mask given here; tests inject the oracle to exercise the gloo path on CPU.
+    and mask given here; tests inject the oracle to run the multi-rank logic on CPU.
     """
 
     def __init__(self, target, H: int, W: int, k_sigma: float = 3.0, weight_mask=None,
                  boost_only: bool = False, group=None, device=None,
-                 evaluate: Optional[Callable[[np.ndarray], np.ndarray]] = None):
-        import torch.distributed as dist
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self.device = device
+                 evaluate: Optional[Callable[[np.ndarray], np.ndarray]] = None, comm=None):
+        self.group, self.device, self.comm, self._own_comm = group, device, comm, False
+        if comm is None and (group is not None or _torch_dist_initialized()):
+            import torch.distributed as dist
+            self.world = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
+        else:
+            if comm is None:
+                from .api import device_index
+                self.comm, self._own_comm = RcclGather(device_index(device)), True
+            self.world, self.rank = int(self.comm.world), int(self.comm.rank)
         if evaluate is None:
             from . import api
             tgt, mask = api.as_f32(target), None if weight_mask is None else api.as_f32(weight_mask)
 
             def evaluate(G):
-                return api.fitness(G, tgt, H, W, k_sigma, weight_mask=mask, boost_only=boost_only)
+                return api.fitness(G, tgt, H, W, k_sigma, weight_mask=mask, boost_only=boost_only,
+                                   device=device)
         self.evaluate = evaluate
 
     def __call__(self, population) -> np.ndarray:
@@ -79,11 +92,52 @@ class ShardedFitness:
         B = len(G)
         b0, b1 = shard_bounds(B, self.world, self.rank)
         local = np.asarray(self.evaluate(G[b0:b1]), np.float32) if b1 > b0 else np.zeros(0, np.float32)
-        return gather_shards(local, B, self.group, self.device)
+        if self.comm is None:
+            return gather_shards(local, B, self.group, self.device)
+        per = -(-B // self.world)                  # equal slots: one all-gather, tail padded
+        send = np.zeros(per, np.float32)
+        send[:len(local)] = local
+        return np.asarray(self.comm.allgather_host(send), np.float32).reshape(-1)[:B]
+
+    def close(self) -> None:
+        if self._own_comm and self.comm is not None:
+            self.comm.close()
+            self.comm = None
 
 
 # ---- torch-free rendezvous -------------------------------------------------------
 _RDZV_SEQ = [0]
+
+
+def _torch_dist_initialized() -> bool:
+    """A torch.distributed default group exists (checked without importing torch)."""
+    d = sys.modules.get("torch.distributed")
+    try:
+        return bool(d is not None and d.is_available() and d.is_initialized())
+    except Exception:  # noqa: BLE001 — a partially imported torch
+        return False
+
+
+def process_start_time(pid: int) -> Optional[float]:
+    """Start time of process ``pid`` in seconds since the epoch (from /proc; 10-ms
+    resolution), None when unknown."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        start_ticks = int(fields[19])                 # field 22 of stat(5)
+        with open("/proc/stat") as f:
+            btime = next(int(line.split()[1]) for line in f if line.startswith("btime"))
+        return btime + start_ticks / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, IndexError, StopIteration):
+        return None
+
+
+def launch_time() -> float:
+    """When this launch began: the launcher (torchrun's agent or bench.py's spawner,
+    the parent of every local rank) started before any rank wrote an id file, so a
+    file older than it is left over from an earlier launch with the same key."""
+    t = process_start_time(os.getppid())
+    return (t - 0.05) if t is not None else 0.0
 
 
 def launch_env():
@@ -111,10 +165,11 @@ def file_rendezvous(rank: int, world: int, make_id, key: Optional[str] = None,
     """Carry the 128-byte RCCL id from rank 0 to the other ranks of THIS node
     without a process group: rank 0 writes it atomically (tmp + rename) to a file
     named by ``key`` and a per-process sequence number (the n-th communicator
-    every rank makes); the others poll for it.  Rank 0 removes the file in
-    ``release_rendezvous`` once the communicator exists (all ranks have read it:
-    RCCL's init is collective).  Single node only — the scope of north_star's
-    8-GPU sharding."""
+    every rank makes); the others poll for it and accept only a file written after
+    the launch began (``launch_time``), so an id left behind by a launch that
+    crashed before rank 0 could remove it is never read.  Rank 0 removes the file
+    once the communicator exists (all ranks have read it: RCCL's init is
+    collective).  Single node only — the scope of north_star's 8-GPU sharding."""
     seq = _RDZV_SEQ[0]
     _RDZV_SEQ[0] += 1
     d = directory or os.environ.get("GGS_RDZV_DIR") or tempfile.gettempdir()
@@ -127,11 +182,13 @@ def file_rendezvous(rank: int, world: int, make_id, key: Optional[str] = None,
         os.replace(tmp, path)
         return idb
     t0 = time.monotonic()
+    fresh_after = launch_time()
     while True:
         try:
             with open(path, "rb") as f:
                 idb = f.read()
-            if len(idb) == 128:
+                mtime = os.fstat(f.fileno()).st_mtime
+            if len(idb) == 128 and mtime >= fresh_after:   # not a crashed launch's left-over
                 return idb
         except FileNotFoundError:
             pass
@@ -162,8 +219,12 @@ class RcclGather:
     def __init__(self, device: int, group=None, rank: Optional[int] = None,
                  world: Optional[int] = None, key: Optional[str] = None):
         from . import _lib
+        self.handle = None
         _lib.preload_rccl()
         self._lib, self._C = _lib, C
+        if group is None and rank is None and world is None and _torch_dist_initialized():
+            import torch.distributed as dist     # an existing process group carries the id
+            group = dist.group.WORLD
         if group is not None:
             import torch.distributed as dist
             self.world = dist.get_world_size(group)
@@ -178,6 +239,12 @@ class RcclGather:
             r, w, _ = launch_env()
             self.rank = r if rank is None else int(rank)
             self.world = w if world is None else int(world)
+            lw = os.environ.get("LOCAL_WORLD_SIZE")
+            if world is None and self.world > 1 and lw is not None and int(lw) != self.world:
+                raise RuntimeError(
+                    f"RcclGather: WORLD_SIZE={self.world} spans more than this node "
+                    f"(LOCAL_WORLD_SIZE={lw}); the file rendezvous is node-local — pass a "
+                    f"torch.distributed `group` (or initialise the default process group) instead")
 
             def make_id():
                 b = (C.c_uint8 * 128)()

@@ -217,6 +217,13 @@ int ggs_sa_read(void* handle, float* current, float* best, float* neighbours);
  * ggs_sa_run or by ggs_sa_propose/commit, not both. */
 int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iters, int32_t tries,
                const double* temps, int32_t width, double* curves_out);
+/* ggs_sa_run's batching rule (pure host arithmetic, no device): rounds enqueued
+ * before the next host sync when `remaining` tries of the chunk are left and a
+ * round is expected to consume `est` of them — ceil(remaining / est), at least
+ * 1, at most GGS_SA_MAX_ROUNDS_PER_SYNC (a bound on the dispatches queued
+ * between syncs: 4 per round, 6 with incremental evaluation). */
+#define GGS_SA_MAX_ROUNDS_PER_SYNC 64
+int64_t ggs_sa_rounds_per_sync(int64_t remaining, int32_t est);
 /* The device loop's state after the last ggs_sa_run (any output may be NULL). */
 int ggs_sa_loop_state(void* handle, double* best_fit, double* curr_fit, uint64_t* rounds,
                       uint64_t* evaluated, uint64_t* accepted);
@@ -225,7 +232,9 @@ int ggs_sa_loop_state(void* handle, double* best_fit, double* curr_fit, uint64_t
 int ggs_sa_accept_uniform(uint64_t seed, int32_t it, int32_t k, double* u);
 /* Incremental evaluation (default off): a neighbour's 16-column strips that no
  * changed splat touches (old or new AABB) keep the current state's partial sums —
- * bit-identical to a full re-render; off = every strip is rasterised. */
+ * bit-identical to a full re-render; off = every strip is rasterised.  Turning
+ * it on re-evaluates the current state's records and strip partials (the device
+ * loop keeps them only while it is on), so it may be toggled between calls. */
 int ggs_sa_set_incremental(void* handle, int32_t on);
 /* Neighbours proposed and splats found changed (summed over proposals). */
 int ggs_sa_stats(void* handle, uint64_t* proposed, uint64_t* changed_splats);

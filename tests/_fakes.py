@@ -1,0 +1,211 @@
+"""CPU stand-ins for the GPU side of the multi-rank path (test infrastructure).
+
+* ``PipeMesh`` / ``PipeComm``: an in-memory all-gather between rank processes
+  over multiprocessing pipes, with the interface of ``ggs.RcclGather``
+  (``rank``, ``world``, ``allgather``, ``wait``, ``allgather_host``, ``barrier``,
+  ``close``).  Its 128-byte id still travels through the REAL
+  ``ggs.parallel.file_rendezvous`` (rank 0 writes, the others poll), and every
+  rank checks that it received rank 0's bytes.  Each message carries
+  (communicator sequence number, call number, kind), so two ranks that issue
+  their collectives in a different order or a different number of times fail
+  loudly instead of pairing the wrong calls.
+* ``install_fake_gpu``: ``ggs`` / ``ggs.hip`` modules whose device memory is a
+  registry of numpy arrays, so ``bench.run()`` executes its whole distributed
+  control flow (rendezvous, ramps, timed passes, max over ranks, shard check,
+  JSON line) on CPU.  The stand-in fitness of a candidate is the float32 sum of
+  its genome; nothing here is the product.
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import sys
+import types
+
+import numpy as np
+
+from conftest import PKG
+
+TIMEOUT_S = 60.0
+
+
+def real_parallel():
+    """ggs/parallel.py itself, loaded from its file (the stand-in ``ggs`` package
+    of ``install_fake_gpu`` would shadow ``ggs.parallel``)."""
+    import importlib.util
+    m = sys.modules.get("_ggs_parallel_real")
+    if m is None:
+        spec = importlib.util.spec_from_file_location("_ggs_parallel_real",
+                                                      os.path.join(PKG, "ggs", "parallel.py"))
+        m = importlib.util.module_from_spec(spec)
+        sys.modules["_ggs_parallel_real"] = m
+        spec.loader.exec_module(m)
+    return m
+
+
+class PipeMesh:
+    """One duplex pipe per rank pair, made in the parent before the fork."""
+
+    def __init__(self, world: int, ctx):
+        self.world = world
+        self.ends = {}
+        for a, b in itertools.combinations(range(world), 2):
+            ea, eb = ctx.Pipe(duplex=True)
+            self.ends[(a, b)], self.ends[(b, a)] = ea, eb
+
+    def peer(self, rank: int, q: int):
+        return self.ends[(rank, q)]
+
+
+class PipeComm:
+    _seq = itertools.count()              # n-th communicator this process made
+
+    def __init__(self, mesh: PipeMesh, rank: int, world: int, log=None, corrupt=False, key=None):
+        file_rendezvous = real_parallel().file_rendezvous
+        self.mesh, self.rank, self.world, self.log = mesh, rank, world, log
+        self.corrupt = corrupt
+        self.cid = next(PipeComm._seq)
+        self.calls = 0
+        self.tickets = {}
+        idb = file_rendezvous(rank, world, lambda: os.urandom(128), key)
+        ids = self._exchange("id", np.frombuffer(idb, np.uint8).copy())
+        assert all(bytes(x) == bytes(ids[0]) for x in ids), "ranks received different communicator ids"
+        self.id = bytes(idb)
+        if log is not None:
+            log.setdefault("comms", []).append({"cid": self.cid, "id": self.id.hex()[:16]})
+
+    def _exchange(self, kind: str, payload: np.ndarray):
+        """Every rank's payload, in rank order (pairwise, lower rank sends first)."""
+        tag = (self.cid, self.calls, kind)
+        self.calls += 1
+        out = [None] * self.world
+        out[self.rank] = payload
+        for q in range(self.world):
+            if q == self.rank:
+                continue
+            c = self.mesh.peer(self.rank, q)
+            msgs = []
+            if self.rank < q:
+                c.send((tag, payload))
+            if not c.poll(TIMEOUT_S):
+                raise TimeoutError(f"rank {self.rank}: no {kind} from rank {q} (call {tag})")
+            msgs.append(c.recv())
+            if self.rank > q:
+                c.send((tag, payload))
+            rtag, data = msgs[0]
+            if rtag != tag:
+                raise AssertionError(f"rank {self.rank} issued {tag} but rank {q} issued {rtag}")
+            out[q] = data
+        return out
+
+    # ---- the RcclGather interface --------------------------------------------------
+    def allgather(self, stream, d_send, d_recv, count, overlap=False):
+        send = MEM[d_send].reshape(-1)[:count].copy()
+        parts = self._exchange("gather", send)
+        recv = MEM[d_recv].reshape(-1)
+        for r, p in enumerate(parts):
+            recv[r * count:(r + 1) * count] = p
+        if self.corrupt:
+            recv[self.rank * count] += 1.0
+        if self.log is not None:
+            g = self.log.setdefault("gathers", {})
+            g[str(self.cid)] = g.get(str(self.cid), 0) + 1
+            self.log["gather_count"] = int(count)
+        if overlap:
+            t = len(self.tickets)
+            self.tickets[t] = True
+            return t
+        return -1
+
+    def wait(self, stream, ticket):
+        if ticket >= 0:
+            assert self.tickets.pop(ticket), "wait on an unknown ticket"
+
+    def allgather_host(self, values):
+        v = np.ascontiguousarray(values, np.float32).reshape(-1)
+        return np.stack(self._exchange("host", v), 0)
+
+    def barrier(self):
+        self._exchange("barrier", np.zeros(0, np.float32))
+
+    def close(self):
+        pass
+
+
+# ---- fake device memory + ggs modules for bench.run() -------------------------------
+MEM = {}
+_ptrs = itertools.count(0x1000, 0x1000)
+
+
+class _DeviceArray:
+    def __init__(self, shape, dtype=np.float32):
+        self.shape = tuple(np.atleast_1d(shape)) if not isinstance(shape, tuple) else shape
+        self.a = np.zeros(self.shape, dtype)
+        self.ptr = next(_ptrs)
+        MEM[self.ptr] = self.a
+
+    @classmethod
+    def from_host(cls, a):
+        d = cls(a.shape, a.dtype)
+        d.a[...] = a
+        return d
+
+    def to_host(self, stream=None):
+        return self.a.copy()
+
+
+class _Stream:
+    _h = itertools.count(1)
+
+    def __init__(self):
+        self.handle = next(self._h)
+
+    def synchronize(self):
+        pass
+
+
+def install_fake_gpu(mesh, rank, world, log, slow_rank=None, corrupt=False):
+    """Put stand-in ``ggs`` and ``ggs.hip`` modules in sys.modules."""
+    import time
+
+    hip = types.ModuleType("ggs.hip")
+    hip.DeviceArray, hip.Stream = _DeviceArray, _Stream
+    hip.set_device = lambda d: log.__setitem__("device", int(d))
+    hip.synchronize = lambda: None
+
+    def memcpy_d2h_async(host, ptr, nbytes, stream):
+        host.reshape(-1).view(np.uint8)[:nbytes] = MEM[ptr].reshape(-1).view(np.uint8)[:nbytes]
+    hip.memcpy_d2h_async = memcpy_d2h_async
+
+    class TargetPlan:
+        def __init__(self, device, stream, d_target, d_mask, mode, beta, H, W):
+            log["plan"] = [int(device), int(H), int(W), int(mode)]
+
+        def fitness_device(self, stream, d_genomes, B, N, Cc, k_sigma, d_out):
+            g = MEM[d_genomes].reshape(-1, N, Cc)
+            assert g.shape[0] == B, (g.shape, B)
+            MEM[d_out].reshape(-1)[:B] = g.reshape(B, -1).sum(1, dtype=np.float32)
+            log.setdefault("batches", set()).add(int(B))
+            if slow_rank == rank:
+                time.sleep(0.001)
+
+    prof = {}
+    ggs = types.ModuleType("ggs")
+    ggs.hip = hip
+    ggs.GGS_FIT_WEIGHTED = 1
+    ggs.ensure_init = lambda: max(world, 1)
+    ggs.select_devices = lambda ids: log.__setitem__("selected", list(ids))
+    ggs.TargetPlan = TargetPlan
+    ggs.RcclGather = lambda local_rank: PipeComm(mesh, rank, world, log, corrupt)
+    ggs.profile_reset = prof.clear
+    ggs.profile_enable = lambda on: None
+    ggs.profile_read = lambda k: (0.1, 1)
+    ggs.encode = lambda G: np.asarray(G, np.float32)
+
+    def preprocess(G, H, W, k):
+        n = int(np.prod(G.shape[:-1]))
+        z = np.zeros(n, np.int32)
+        return {"x0": z, "x1": z + 3, "y0": z, "y1": z + 3}
+    ggs.preprocess = preprocess
+    sys.modules["ggs"], sys.modules["ggs.hip"] = ggs, hip
+    return ggs

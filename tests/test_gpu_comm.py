@@ -178,3 +178,44 @@ def test_device_ga_sharded_over_world1_comm_is_the_plain_ga(hip, via, monkeypatc
     np.testing.assert_array_equal(a["population"], b["population"])
     np.testing.assert_array_equal(a["fitness"], b["fitness"])
     assert a["best_fit"] == b["best_fit"] and a["curves"] == b["curves"]
+
+
+def test_configs3_sharded_over_eight_slots_equals_unsharded(hip, monkeypatch):
+    """BASELINE configs[3] on one GPU: 1024^2, 1024 splats, pop 4096 split into the
+    8 contiguous shards of an 8-rank job (``shard_bounds(4096, 8, r)``).  Each
+    slot evaluates its shard straight into its offset of ONE gather buffer and
+    runs its world-1 RCCL in-place all-gather there (the per-rank step of the
+    8-GPU job, the device GA's layout).  The assembled vector equals the
+    unsharded host-API ``ggs.fitness`` of all 4096 bit for bit, and the first and
+    last candidates of two shards match the oracle (fitness.py:34-47)."""
+    monkeypatch.setenv("GGS_COMM_RCCL_SELF", "1")       # world 1 through RCCL, not the copy kernel
+    from ggs.parallel import shard_bounds
+    H = W = 1024
+    B, N, world = 4096, 1024, 8
+    pop = O.synthetic_population(B, N, H, W, seed=33)
+    rng = np.random.default_rng(34)
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
+    whole = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask, device=0)     # unsharded
+
+    g, t_d, m_d = (hip.DeviceArray.from_host(a) for a in (pop, tgt, mask))
+    gath = hip.DeviceArray.from_host(np.full(B, np.nan, np.float32))
+    st = hip.Stream()
+    plan = ggs.TargetPlan(0, st.handle, t_d.ptr, m_d.ptr, ggs.GGS_FIT_WEIGHTED, 1.0, H, W)
+    comms = [ggs.RcclGather(0, rank=0, world=1) for _ in range(world)]
+    try:
+        spans = [shard_bounds(B, world, r) for r in range(world)]
+        assert [b1 - b0 for b0, b1 in spans] == [512] * world
+        for r, (b0, b1) in enumerate(spans):
+            slot = gath.ptr + 4 * b0
+            plan.fitness_device(st.handle, g.ptr + 4 * 9 * N * b0, b1 - b0, N, 9, 3.0, slot)
+            comms[r].allgather(st.handle, slot, slot, b1 - b0)                 # in place
+        got = gath.to_host(st)
+    finally:
+        for c in comms:
+            c.close()
+        plan.close()
+    np.testing.assert_array_equal(got, whole)
+    picks = [spans[0][0], spans[0][1] - 1, spans[world - 1][0], spans[world - 1][1] - 1]
+    ref = np.asarray(O.fitness_many([pop[i] for i in picks], tgt, H, W, 3.0, weight_mask=mask))
+    assert np.max(np.abs(got[picks] - ref) / np.abs(ref)) <= 1e-5

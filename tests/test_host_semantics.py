@@ -167,3 +167,31 @@ def test_sa_accept_uniform_is_philox():
         assert all(0.0 <= u < 1.0 for u in us) and len(set(us)) == len(us)
     with pytest.raises(Exception):
         PhiloxAcceptDraws(0).accept_at(-1, 0)
+
+
+def test_host_api_reselects_after_a_direct_select_devices(monkeypatch):
+    """``ggs.select_devices`` and the host API share one view of the library's
+    device list: after a direct selection the next call re-selects its own
+    device, and the selection and the call happen under one lock."""
+    from ggs import _lib, api
+    calls = []
+
+    class FakeLib:
+        def ggs_select_devices(self, arr, n):
+            calls.append([arr[i] for i in range(n)])
+            assert _lib.device_lock._is_owned()
+            return n
+
+    monkeypatch.setattr(_lib, "lib", FakeLib())
+    monkeypatch.setattr(_lib, "ensure_init", lambda: 2)
+    monkeypatch.setattr(_lib, "selected", [None])
+    with api._on_devices("cuda:0", 1) as nd:
+        assert nd == 1 and _lib.device_lock._is_owned()
+    with api._on_devices(0, 1):
+        pass                                   # cached: no second selection
+    _lib.select_devices([1])                   # a caller points the library elsewhere
+    with api._on_devices(0, 1):
+        pass
+    with api._on_devices(None, 0) as nd:       # all devices
+        assert nd == 2
+    assert calls == [[0], [1], [0], [0, 1]]

@@ -119,3 +119,26 @@ def test_sa_rejects_inconsistent_loop_arguments(kw):
                               CFG["mut_sigma_min"], "cosine", MIN_S, MAX_S, 3.0, 0.7, False, 2,
                               1e-3, "cosine", 2, evaluate=never if kw.get("backend") == "host" else None,
                               progress=False, **kw)
+
+
+def test_device_loop_batching_rule_is_bounded():
+    """ggs_sa_run's rounds per host sync (ggs_sa_rounds_per_sync, pure host
+    arithmetic): enough rounds to finish the chunk at the expected consumption
+    (never past it), at least one, and never more than GGS_SA_MAX_ROUNDS_PER_SYNC
+    — an unbounded batch (~1,000 rounds = 4,000 queued dispatches at high
+    acceptance) crashed the launch under rocprofv3 --pmc."""
+    import re
+    from conftest import REPO
+    from ggs import lib
+    cap = int(re.search(r"#define GGS_SA_MAX_ROUNDS_PER_SYNC (\d+)",
+                        open(f"{REPO}/include/ggs.h").read()).group(1))
+    assert 16 <= cap <= 256
+    f = lib.ggs_sa_rounds_per_sync
+    for remaining in (0, 1, 7, 8, 63, 64, 65, 2048, 16_000, 2**31 - 1):
+        for est in (-3, 0, 1, 2, 3, 16, 64, 10_000):
+            R = f(remaining, est)
+            e = max(1, est)
+            assert 1 <= R <= cap
+            assert R == max(1, min(cap, -(-max(remaining, 0) // e)))
+            assert (R - 1) * e < max(remaining, 1)      # the batch never starts a round past the chunk
+    assert f(2048, 2) == cap and f(16_000, 16) == cap   # the crashing regimes are capped
