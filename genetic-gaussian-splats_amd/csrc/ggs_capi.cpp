@@ -1516,6 +1516,24 @@ int ggs_sa_commit(void* handle, int32_t j, int32_t update_best) {
     return GGS_OK;
 }
 
+int64_t ggs_sa_rounds_per_sync(int64_t remaining, int32_t est) {
+    const int64_t e = std::max<int64_t>(1, est);
+    const int64_t R = std::max<int64_t>(1, (std::max<int64_t>(remaining, 0) + e - 1) / e);
+    return std::min<int64_t>(R, GGS_SA_MAX_ROUNDS_PER_SYNC);
+}
+
+// Diagnostic override of the bound (tools/probe/sa_pmc_r03b.sh reproduces the
+// round-2 crash with it lifted); not part of the C ABI.
+static int64_t sa_rounds_per_sync(int64_t remaining, int32_t est) {
+    static const int64_t cap = [] {
+        const char* v = getenv("GGS_SA_MAX_ROUNDS_PER_SYNC");
+        return v ? std::max<int64_t>(1, atoll(v)) : (int64_t)0;
+    }();
+    if (!cap) return ggs_sa_rounds_per_sync(remaining, est);
+    const int64_t e = std::max<int64_t>(1, est);
+    return std::min<int64_t>(cap, std::max<int64_t>(1, (std::max<int64_t>(remaining, 0) + e - 1) / e));
+}
+
 int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iters, int32_t tries,
                const double* temps, int32_t width, double* curves_out) {
     if (!handle) return fail(GGS_EINVAL, "null handle");
@@ -1608,7 +1626,7 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
     int est = width > 0 ? width : (s->h_loop->acc_rate < 1.0 / s->cap ? s->cap
                                    : std::max(1, (int)lrint(1.0 / s->h_loop->acc_rate)));
     for (;;) {
-        const int64_t R = ggs_sa_rounds_per_sync(remaining, est);
+        const int64_t R = sa_rounds_per_sync(remaining, est);
         for (int64_t r = 0; r < R; ++r)
             if ((rc = round())) return rc;
         GGS_HIP(hipMemcpyAsync(s->h_loop, loop, sizeof(SaLoopDev), hipMemcpyDeviceToHost, s->st));
@@ -1646,12 +1664,6 @@ int ggs_sa_accept_uniform(uint64_t seed, int32_t it, int32_t k, double* u) {
     if (!u || it < 0 || k < 0) return fail(GGS_EINVAL, "bad arguments");
     *u = sa_accept_uniform(seed, (uint32_t)it, (uint32_t)k);
     return GGS_OK;
-}
-
-int64_t ggs_sa_rounds_per_sync(int64_t remaining, int32_t est) {
-    const int64_t e = std::max<int64_t>(1, est);
-    const int64_t R = std::max<int64_t>(1, (std::max<int64_t>(remaining, 0) + e - 1) / e);
-    return std::min<int64_t>(R, GGS_SA_MAX_ROUNDS_PER_SYNC);
 }
 
 int ggs_sa_set_incremental(void* handle, int32_t on) {
