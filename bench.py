@@ -103,17 +103,18 @@ def synthetic_population(B, N, seed):
     return G
 
 
-def _bench_profiles():
-    """profiles/rNN/summary.json of this workload, oldest round first (the
-    profiles/rNN_<config> directories hold the other configs)."""
+def _bench_profiles(config="512"):
+    """profiles/rNN/summary.json of the headline workload (config "512"), or
+    profiles/rNN_<config>/summary.json of another bench config, oldest round first."""
     import glob
     import re
+    pat = r"r\d+" if config == "512" else r"r\d+_" + re.escape(config)
     return sorted(p for p in glob.glob(os.path.join(REPO, "profiles", "r*", "summary.json"))
-                  if re.fullmatch(r"r\d+", os.path.basename(os.path.dirname(p))))
+                  if re.fullmatch(pat, os.path.basename(os.path.dirname(p))))
 
 
-def _summary():
-    paths = _bench_profiles()
+def _summary(config="512"):
+    paths = _bench_profiles(config)
     if not paths:
         return None, None
     try:
@@ -122,22 +123,22 @@ def _summary():
         return None, None
 
 
-def pmc_traffic():
+def pmc_traffic(config="512"):
     """HBM bytes per raster launch from the newest committed rocprofv3 PMC
-    summary of this same workload (tools/profile.sh -> profiles/rNN/summary.json:
-    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE); None when absent."""
-    d, src = _summary()
+    summary of this same workload (tools/profile.sh -> profiles/rNN[_<config>]/
+    summary.json: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE); None when absent."""
+    d, src = _summary(config)
     try:
         return d["raster_hbm_bytes_per_launch"]["total"], src
     except (TypeError, KeyError):
         return None, None
 
 
-def pmc_valu_busy():
+def pmc_valu_busy(config="512"):
     """Fraction of SIMD cycles the raster kernel's VALU was busy, from the same
     committed PMC summary: SQ_ACTIVE_INST_VALU (quad-cycles, summed over SIMDs)
     x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); None when absent."""
-    d, _ = _summary()
+    d, _ = _summary(config)
     try:
         cs = d["counters"]
         c = cs[next(k for k in cs if "raster_kernel<1" in k)]
@@ -146,15 +147,26 @@ def pmc_valu_busy():
         return None
 
 
-def pmc_trace_avg_us():
+def pmc_trace_avg_us(config="512"):
     """The committed rocprofv3 kernel-trace average of the raster kernel over a
     single-stream bench pass (tools/profile.sh runs bench.py --streams 1)."""
-    d, _ = _summary()
+    d, _ = _summary(config)
     try:
         return d.get("raster_profile_pass_avg_us") or \
             next(v["avg_us"] for k, v in d["kernels"].items() if "raster_kernel<1" in k)
     except (AttributeError, StopIteration, KeyError):
         return None
+
+
+def profile_config(config, pop_arg, per_gpu):
+    """The bench config whose committed profile has this launch's shape: the config
+    itself at its own batch; else the config launching the same (size, splats,
+    candidates per GPU) — configs[3] split over 8 ranks is configs[2]'s launch;
+    None for a --pop exploration nothing profiled."""
+    Hc, Nc, Pc, _ = CONFIGS[config]
+    if pop_arg <= 0 and per_gpu == Pc:
+        return config
+    return next((c for c, v in CONFIGS.items() if v[:3] == (Hc, Nc, per_gpu)), None)
 
 
 # ---- CPU baseline -----------------------------------------------------------------
@@ -471,6 +483,35 @@ def run(args, world, rank, local_rank, distributed):
         rb_s = max_over_ranks([(time.perf_counter() - t0) / n_rb])[0]
         extras["value_with_readback"] = round(world * POP / rb_s, 1)
         barrier()
+
+        # The timed step excludes the target plan (built once above, as the device GA
+        # does for its fixed target).  A caller of the plain device API
+        # (ggs_fitness_device) rebuilds it on every call: its one-stream rate, and the
+        # plan build alone (host-timed around a synchronised ggs_plan_create).
+        ramp(args.ramp_ms / 3, 1)
+        t0, n_u = time.perf_counter(), 0
+        while time.perf_counter() - t0 < args.min_time:
+            for i in range(args.steps):
+                ggs.fitness_device(local_rank, sts[0], pops[i % N_POPS].ptr, POP, N_SPLATS, 9, tgt.ptr,
+                                   mask.ptr, ggs.GGS_FIT_WEIGHTED, 1.0, H, W, K_SIGMA, outs[i % RING].ptr)
+            streams[0].synchronize()
+            n_u += args.steps
+        un_s = max_over_ranks([(time.perf_counter() - t0) / n_u])[0]
+        builds = []
+        for _ in range(6):
+            t1 = time.perf_counter()
+            p2 = ggs.TargetPlan(local_rank, sts[0], tgt.ptr, mask.ptr, ggs.GGS_FIT_WEIGHTED, 1.0, H, W)
+            streams[0].synchronize()
+            builds.append(time.perf_counter() - t1)
+            p2.close()
+        extras["plan_excluded"] = {
+            "note": "the timed step reuses one target plan (ggs_plan_create, once per target/mask/mode); "
+                    "ggs_fitness_device rebuilds it per call",
+            "plan_build_ms": round(float(np.median(builds[1:])) * 1e3, 4),
+            "device_api_unplanned_value": round(world * POP / un_s, 1),
+            "device_api_unplanned_ms_per_step": round(un_s * 1e3, 4),
+            "excluded_ms_per_step": round(un_s * 1e3 - elapsed1 / args.steps * 1e3, 4)}
+        barrier()
         ramp(args.ramp_ms / 3, 1)
 
         # per-kernel device time (HIP events on the launch stream) over a single-stream
@@ -513,7 +554,12 @@ def run(args, world, rank, local_rank, distributed):
     if kern:
         raster_ms = kern["raster"][0] / max(kern["raster"][1], 1)
         achieved = step_bytes / (raster_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic() if headline else (None, None)
+        # PMC figures of a committed profile with this launch's shape (profiles/rNN or
+        # rNN_<config>): configs[3] split over 8 ranks launches configs[2]'s 512 per GPU;
+        # a --pop exploration has none
+        prof_cfg = profile_config(args.config, args.pop, POP)
+        profiled = prof_cfg is not None
+        traffic, traffic_src = pmc_traffic(prof_cfg) if profiled else (None, None)
         valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
         roof = {"bound": "hbm", "kernel": "raster_kernel<1, false>" if N_SPLATS <= 512 else
                 "raster_kernel<1, true>",
@@ -526,8 +572,12 @@ def run(args, world, rank, local_rank, distributed):
                 "regime": "single-stream pass (kernels alone, HIP events on the launch stream); pairs "
                           "with ms_per_step_one_stream, as the committed rocprofv3 trace (bench.py "
                           "--streams 1)",
-                "rocprof_trace_avg_ms": (None if not headline or pmc_trace_avg_us() is None
-                                         else round(pmc_trace_avg_us() / 1e3, 5)),
+                "rocprof_trace_avg_ms": (None if not profiled or pmc_trace_avg_us(prof_cfg) is None
+                                         else round(pmc_trace_avg_us(prof_cfg) / 1e3, 5)),
+                # the roof that binds: the VALU; frac above is
+                # the HBM fraction the contract asks for, not the limiter
+                "binding": "valu",
+                "binding_busy_pmc": pmc_valu_busy(prof_cfg) if profiled else None,
                 "step_effective": {"regime": f"headline, {args.streams} streams (overlapping batches)",
                                    "achieved": round(step_bytes / (ms_step * 1e-3) / 1e9, 2),
                                    "frac": round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
@@ -538,7 +588,7 @@ def run(args, world, rank, local_rank, distributed):
                 "flop_per_aabb_pair": FLOP_PER_PAIR, "aabb_pairs_per_candidate": pairs_per_cand,
                 "accounting": "reference-equivalent work: 24 FLOP per AABB pair (SURVEY.md §8d); "
                               "the row recurrence executes fewer, so frac can exceed 1",
-                "busy_pmc": pmc_valu_busy() if headline else None}
+                "busy_pmc": pmc_valu_busy(prof_cfg) if profiled else None}
     if rank == 0:
         line = {
             "metric": METRIC if headline else

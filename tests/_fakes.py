@@ -196,6 +196,11 @@ def install_fake_gpu(mesh, rank, world, log, slow_rank=None, corrupt=False):
     ggs.ensure_init = lambda: max(world, 1)
     ggs.select_devices = lambda ids: log.__setitem__("selected", list(ids))
     ggs.TargetPlan = TargetPlan
+    TargetPlan.close = lambda self: None
+
+    def fitness_device(dev, st, d_gen, B, N, Cc, d_t, d_m, mode, beta, H, W, k, d_out):
+        TargetPlan(dev, st, d_t, d_m, mode, beta, H, W).fitness_device(st, d_gen, B, N, Cc, k, d_out)
+    ggs.fitness_device = fitness_device
     ggs.RcclGather = lambda local_rank: PipeComm(mesh, rank, world, log, corrupt)
     ggs.profile_reset = prof.clear
     ggs.profile_enable = lambda on: None

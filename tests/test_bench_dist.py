@@ -87,6 +87,9 @@ def test_bench_world2_orchestration(tmp_path):
     assert line["config"]["rccl_ranks"] == 2 and line["config"]["global_batch"] == 256
     assert line["config"]["fitness_gather"] == "rccl" and line["config"]["pop_per_gpu"] == 128
     assert line["timing"]["passes"] >= 1 and line["value"] > 0
+    assert line["roofline"]["binding"] == "valu" and line["roofline"]["bound"] == "hbm"
+    pe = line["plan_excluded"]
+    assert pe["device_api_unplanned_value"] > 0 and pe["plan_build_ms"] >= 0
     assert not (tmp_path / "stdout1.txt").read_text().strip()               # rank 1 prints nothing
 
 

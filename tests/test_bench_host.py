@@ -124,3 +124,12 @@ def test_visible_gpus_honours_visible_devices_lists(monkeypatch):
 def test_cpu_cores_respects_the_job_share(monkeypatch):
     monkeypatch.setenv("OMP_NUM_THREADS", "3")
     assert bench.cpu_cores() == min(3, len(os.sched_getaffinity(0)))
+
+
+def test_profile_config_matches_the_launch_shape():
+    assert bench.profile_config("512", 0, 128) == "512"
+    assert bench.profile_config("1024", 0, 512) == "1024"
+    assert bench.profile_config("1024x8", 0, 4096) == "1024x8"       # N = 1: the whole population
+    assert bench.profile_config("1024x8", 0, 512) == "1024"          # N = 8: configs[2]'s launch
+    assert bench.profile_config("1024x8", 0, 2048) is None           # N = 2: not profiled
+    assert bench.profile_config("512", 64, 64) is None               # --pop exploration
