@@ -192,6 +192,12 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
         R2 = R2 * (f2_t)s.rho;                                                       \
         GGS_BLEND(k, F2);                                                            \
     }
+// The first pair's ratio to the next: 2^d, d(qy) = 16 Cc (qy + 4) + 8 bx.  Live
+// lanes have d <= -e(seed) <= 100 (make_rec's seed guard: e <= 0 everywhere), so
+// the clamp is exact there; dead lanes (px = -inf, f = 0) only need a finite
+// ratio (0 * r = 0), which the clamp gives without a per-lane select (round 3:
+// raster -1.0 %, bit-identical).
+#define GGS_RATIO(qy) GGS_EXP2(fminf(__builtin_fmaf((qy), s.c16, 8.0f * bx), 100.0f))
 #define GGS_FOR8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #define GGS_FOR16P(X) GGS_FOR8(X) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
@@ -343,8 +349,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
                 }
                 GGS_BLEND(0, F2);
                 // d(qy) = 16 Cc (qy + 4) + 8 bx; the .y row's ratio is 2^(64 Cc) times it
-                const float t8_ = px > -__builtin_inff() ? 8.0f * bx : -__builtin_inff();
-                R2.x = GGS_EXP2(__builtin_fmaf(qyv.y, s.c16, t8_));
+                R2.x = GGS_RATIO(qyv.y);
                 R2.y = R2.x * __builtin_fabsf(s.rho4);
 #define GGS_FULL(k)                                                                     \
     if ((k) >= 1 && (k) < NPK - 1) {                                                    \
@@ -387,10 +392,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
                 __ballot((px > -__builtin_inff()) &                                     \
                          (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u))) \
                 goto x##k;                                                              \
-            /* live lanes: d <= -e(seed) <= 100; dead lanes: d = -inf -> r = 0;  */     \
             /* d(qy) = 16 Cc (qy + 4) + 8 bx, the .y row's ratio 2^(64 Cc) times */     \
-            const float t8_ = px > -__builtin_inff() ? 8.0f * bx : -__builtin_inff();  \
-            R2.x = GGS_EXP2(__builtin_fmaf(qy_.y, s.c16, t8_));                         \
+            R2.x = GGS_RATIO(qy_.y);                                                    \
             R2.y = R2.x * __builtin_fabsf(s.rho4);                                      \
             goto u##k;                                                                  \
         }                                                                               \
