@@ -13,12 +13,13 @@ namespace ggs {
 // r, g, b: colour in [0,1] (render.py:40-42); x0..y1: inclusive integer AABB
 // (render.py:27-30).
 struct __attribute__((aligned(16))) SplatRec {
-    // Cc, r, g, b, rho sit in odd dwords: the raster broadcasts them to both halves
-    // of its v_pk_* ops straight from the record's SGPR pair (op_sel hi) instead of
-    // copying each into a pair of its own per visit.
-    float cx, Cc, cy, r;
-    float A, g, Bc, b;
-    float la, rho, c16, rho4;  // row-recurrence constants: 2^(128 Cc), 16 Cc, 2^(64 Cc) (8-row step)
+    // Cc, r, g, b, rho and c16 sit in EVEN dwords: a 16-dword s_load lands them in
+    // even SGPRs, the low half of an aligned SGPR pair, which the raster's v_pk_*
+    // ops broadcast to both halves (op_sel_hi) with no per-visit copy (round 3:
+    // raster -2.8 % vs odd dwords, which the compiler copied into even SGPRs).
+    float Cc, cx, r, cy;
+    float g, A, b, Bc;
+    float rho, la, c16, rho4;  // row-recurrence constants: 2^(128 Cc), 16 Cc, 2^(64 Cc) (8-row step)
     int x0, x1, y0, y1;
 };
 static_assert(sizeof(SplatRec) == 64, "SplatRec must be 64 bytes");
