@@ -115,9 +115,6 @@ constexpr int SAT_MIN_SPLATS = 512;          // launches with fewer splats use t
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-#ifndef GGS_TOPFREE
-#define GGS_TOPFREE 0
-#endif
 #ifndef GGS_TIMING
 #define GGS_TIMING 0              // diagnostic build: per-wave phase clocks (tools/probe/wave_timing.py)
 #endif
@@ -369,9 +366,6 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             }
             // about half the partial visits start at the tile's top (the splat began
             // in a tile above): test that before the switch's compare tree
-#if GGS_TOPFREE
-            if (y0 <= ty0) goto t0;      // began in a tile above: no top row mask
-#endif
             if (kA == 0) goto f0;
             switch (kA) {
 #define GGS_FIRST(k)                                                                    \
@@ -413,29 +407,6 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #undef GGS_FIRST
                 default: __builtin_unreachable();
             }
-#if GGS_TOPFREE
-        t0: {         // first pair 0, rows from the tile's top: only a bottom limit if kB == 0
-            const f2_t e_ = fma2(qyv, fma2((f2_t)s.Cc, qyv, bx2), px2);
-            F2.x = GGS_EXP2(e_.x);
-            F2.y = GGS_EXP2(e_.y);
-            if (kB == 0) {
-                const PairLanes bot_ = rows_upto(y1 - ty0);
-                f2_t fu_;
-                fu_.x = keep_if(bot_.x, F2.x);
-                fu_.y = keep_if(bot_.y, F2.y);
-                GGS_BLEND(0, fu_);
-                goto done;
-            }
-            GGS_BLEND(0, F2);
-            if ((__float_as_uint(s.rho4) >> 31) &&
-                __ballot((px > -__builtin_inff()) &
-                         (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u)))
-                goto x0;
-            R2.x = GGS_RATIO(qyv.y);
-            R2.y = R2.x * __builtin_fabsf(s.rho4);
-            goto u0;
-        }
-#endif
             // recurrence walk: f *= r, r *= rho (no exp).  Two pairs per basic
             // block (the walk's scalar branches split blocks), so the scheduler
             // overlaps one pair's blend with the next pair's recurrence
