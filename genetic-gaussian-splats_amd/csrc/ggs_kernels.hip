@@ -128,24 +128,21 @@ __device__ unsigned long long g_ggs_timing[8 * GGS_TIMING_WAVES];
 #define GGS_TMARK(v)
 #endif
 
-// Row limits as wave lane masks.  Lane l owns row phase ph = l >> 4, so "the
-// lane's row in this pair is >= / <= a wave-uniform bound" is a contiguous range
-// of 16-lane blocks: built on the SALU (one 64-bit shift serves both rows of the
-// pair: s_lshl/s_lshr_b64 take the shift mod 64), applied by one v_cndmask with
-// an SGPR-pair condition — no per-lane compare.
+// Row limits as wave lane masks.  Lane l owns row phase ph = l >> 4: the rows of
+// pair k are 8k + ph (x) and 8k + 4 + ph (y).  Each mask is one per-lane compare
+// writing an SGPR pair, applied by one v_cndmask (round 3: -0.6 % raster vs
+// building the same masks from shifts and selects on the SALU).
 struct PairLanes { uint64_t x, y; };          // rows 8k+ph (x) and 8k+4+ph (y)
 // j = y0 - (ty0 + 8k) <= 7: keep lanes whose row >= y0 (ph >= j, ph + 4 >= j)
-__device__ __forceinline__ PairLanes rows_from(int j) {
-    const int jc = max(j, 0);
-    const uint64_t t = ~0ull << ((16 * jc) & 63);
-    return {jc < 4 ? t : 0ull, jc < 4 ? ~0ull : t};
+__device__ __forceinline__ PairLanes rows_from_ph(int j, int ph) {
+    return {(uint64_t)__ballot(ph >= j), (uint64_t)__ballot(ph + 4 >= j)};
 }
 // m = y1 - (ty0 + 8k) >= 0: keep lanes whose row <= y1 (ph <= m, ph + 4 <= m)
-__device__ __forceinline__ PairLanes rows_upto(int m) {
-    const int mc = min(m, 7);
-    const uint64_t u = ~0ull >> ((48 - 16 * mc) & 63);
-    return {mc >= 3 ? ~0ull : u, mc >= 4 ? u : 0ull};
+__device__ __forceinline__ PairLanes rows_upto_ph(int m, int ph) {
+    return {(uint64_t)__ballot(ph <= m), (uint64_t)__ballot(ph + 4 <= m)};
 }
+#define rows_from(j) rows_from_ph((j), ph)
+#define rows_upto(m) rows_upto_ph((m), ph)
 __device__ __forceinline__ float keep_if(uint64_t lanes, float f) {
     return __builtin_amdgcn_inverse_ballot_w64(lanes) ? f : 0.0f;
 }
