@@ -95,8 +95,16 @@ constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
 constexpr int OCC = 3;            // waves per SIMD the register budget is sized for (<= 168 VGPRs)
 // candidate rotation across the XCDs advances every 2^XCD_SHIFT strip groups (see the grid order)
+// (launches with N > SAT_MIN_SPLATS, the raster_kernel<M, true> instances; the others
+// rotate every group: at 512^2/256 splats the whole launch's records (2.1 MB) and the
+// 4-MiB target plan share each XCD's L2, and rotating every group lets each XCD read
+// each strip's plan slice once: 54 vs 80 MB of fabric traffic per launch, raster
+// -0.5 %; at 1024^2/1024 (33 MB of records) the 8-group rotation is 0.6 % faster)
 constexpr int XCD_SHIFT = 3;
-constexpr int CULL_PRIO = 2;      // s_setprio while culling (1 and 3 measured the same)
+constexpr int CULL_PRIO = 2;
+#ifndef GGS_NOPLAN
+#define GGS_NOPLAN 0      // diagnostic build (tools/probe/traffic_ab.sh): the epilogue reads no plan
+#endif      // s_setprio while culling (1 and 3 measured the same)
 
 // Saturation cut-off.  Front to back, a strip's pixels receive Σ_rest T·f·c +
 // T_end·bg ≤ T from all the splats still to come (Σ w + T_end = T, c, bg ≤ 1).
@@ -237,11 +245,10 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     // candidates rotate by one per group: with B % 8 == 0 a fixed b would stay on
     // one XCD (blocks go round-robin to the 8 XCDs) and per-XCD work would be the
     // sum of 16 candidates' costs (tools/probe/wave_timing.py: XCD end times 197-207 us)
-    // ... but only every 2^XCD_SHIFT groups: blocks B apart (the next group's
-    // block in the same XCD slot) then run the same candidate, whose records stay
-    // in that XCD's caches across 8 groups (raster -0.5 %, one stream +0.7 %;
-    // shifts 2-5 measured alike, 0 = rotate every group)
-    const int b = (int)((blockIdx.x + (gi >> XCD_SHIFT)) % B);
+    // ... for the large-N instances only every 2^XCD_SHIFT groups: blocks B apart
+    // (the next group's block in the same XCD slot) then run the same candidate,
+    // whose records stay in that XCD's caches across 8 groups (see XCD_SHIFT)
+    const int b = (int)((blockIdx.x + (gi >> (SAT ? XCD_SHIFT : 0))) % B);
     const int t = grp / SPB;
     const int wv = (grp % SPB) * WPB + wib;           // strip 0..3 of the tile
     const int tx0 = (t % nTX) * TILE;
@@ -536,7 +543,11 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         const uint64_t bg2b = (uint64_t)__float_as_uint(bg_b) * 0x100000001ull;
 #pragma unroll
         for (int k = 0; k < NPK; ++k) {
+#if GGS_NOPLAN     // traffic probe only (wrong fitness): the epilogue reads no plan
+            const float4 qa = make_float4(0.5f, 0.5f, 0.5f, 0.5f), qb = qa;
+#else
             const float4 qa = P[(2 * k) * 64], qb = P[(2 * k + 1) * 64];
+#endif
             // packed: one v_pk_fma_f32 with the clamp bit per channel and row pair
             // (the compiler folds the clamp only into the scalar v_fma_f32)
             const f2_t T2 = {T[2 * k], T[2 * k + 1]};
@@ -738,12 +749,13 @@ hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_
                        int W, float k, SplatRec* recs, int4* bnds, float* f9, int* i4, float* enc9, const int* live,
                        int n_per) {
     if (S <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)((S + 255) / 256);
+    constexpr int PB = 256;           // 64-thread blocks (all CUs busy): no change, round 3
+    const unsigned grid = (unsigned)((S + PB - 1) / PB);
     if (encode)
-        hipLaunchKernelGGL(prep_kernel<true>, dim3(grid), dim3(256), 0, st, genomes, S, C, H, W, k,
+        hipLaunchKernelGGL(prep_kernel<true>, dim3(grid), dim3(PB), 0, st, genomes, S, C, H, W, k,
                            recs, bnds, f9, i4, enc9, live, n_per);
     else
-        hipLaunchKernelGGL(prep_kernel<false>, dim3(grid), dim3(256), 0, st, genomes, S, C, H, W, k,
+        hipLaunchKernelGGL(prep_kernel<false>, dim3(grid), dim3(PB), 0, st, genomes, S, C, H, W, k,
                            recs, bnds, f9, i4, enc9, live, n_per);
     return hipGetLastError();
 }
