@@ -102,6 +102,9 @@ constexpr int OCC = 3;            // waves per SIMD the register budget is sized
 // -0.5 %; at 1024^2/1024 (33 MB of records) the 8-group rotation is 0.6 % faster)
 constexpr int XCD_SHIFT = 3;
 constexpr int CULL_PRIO = 2;
+#ifndef GGS_ASMX
+#define GGS_ASMX 0
+#endif
 #ifndef GGS_NOPLAN
 #define GGS_NOPLAN 0      // diagnostic build (tools/probe/traffic_ab.sh): the epilogue reads no plan
 #endif      // s_setprio while culling (1 and 3 measured the same)
@@ -168,7 +171,7 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 #define GGS_PK(k, MASKED)                                                            \
     do {                                                                             \
         const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                   \
-        f2_t e_ = fma2(qy_, fma2((f2_t)s.Cc, qy_, bx2), px2);                               \
+        f2_t e_ = GGS_E1(qy_);                                                       \
         if (MASKED) {                                                                \
             if ((unsigned)(8 * (k) - rlo) > rspan) e_.x = -__builtin_inff();         \
             if ((unsigned)(8 * (k) + 4 - rlo) > rspan) e_.y = -__builtin_inff();     \
@@ -203,6 +206,21 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 // ratio (0 * r = 0), which the clamp gives without a per-lane select (round 3:
 // raster -1.0 %, bit-identical).
 #define GGS_RATIO(qy) GGS_EXP2(fminf(__builtin_fmaf((qy), s.c16, 8.0f * bx), 100.0f))
+// The first pair's exponent e = qy (Cc qy + bx) + px for both rows of the pair.
+#if GGS_ASMX
+// Cc broadcast from the low half of the record's (Cc, cx) SGPR pair and bx, px
+// from the low half of VGPR pairs whose high half is never set (op_sel_hi 0): no
+// per-visit broadcast copies of bx and px
+#define GGS_E1(qy) ({                                                                     \
+        f2_t t_, e2_, bxu_, pxu_;                                                         \
+        bxu_.x = bx; pxu_.x = px;                                                         \
+        const uint64_t ccp_ = *reinterpret_cast<const uint64_t*>(&s.Cc);                  \
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(t_) : "s"(ccp_), "v"(qy), "v"(bxu_)); \
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(e2_) : "v"(qy), "v"(t_), "v"(pxu_)); \
+        e2_; })
+#else
+#define GGS_E1(qy) fma2((qy), fma2((f2_t)s.Cc, (qy), bx2), px2)
+#endif
 #define GGS_FOR8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #define GGS_FOR16P(X) GGS_FOR8(X) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
@@ -344,7 +362,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             // test: one straight-line block, the same arithmetic as the general
             // walk (kA = 0, kB = NPK-1, all-ones masks), so the same bits.
             if (max(dy0, TILE_H - 1 - dy1) <= 0) {            // y0 <= ty0 and y1 >= ty0 + 127
-                const f2_t e_ = fma2(qyv, fma2((f2_t)s.Cc, qyv, bx2), px2);
+                const f2_t e_ = GGS_E1(qyv);
                 F2.x = GGS_EXP2(e_.x);
                 F2.y = GGS_EXP2(e_.y);
                 if ((__float_as_uint(s.rho4) >> 31) &&          // only flagged splats (make_rec)
@@ -377,7 +395,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     f##k: __attribute__((unused));                                                      \
         if (k < NPK) {                                                                  \
             const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                  \
-            const f2_t e_ = fma2(qy_, fma2((f2_t)s.Cc, qy_, bx2), px2);                        \
+            const f2_t e_ = GGS_E1(qy_);                                                \
             F2.x = GGS_EXP2(e_.x);                                                      \
             F2.y = GGS_EXP2(e_.y);                                                      \
             f2_t fu_;                                                                   \
