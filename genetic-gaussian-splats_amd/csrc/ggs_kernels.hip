@@ -102,9 +102,6 @@ constexpr int OCC = 3;            // waves per SIMD the register budget is sized
 // -0.5 %; at 1024^2/1024 (33 MB of records) the 8-group rotation is 0.6 % faster)
 constexpr int XCD_SHIFT = 3;
 constexpr int CULL_PRIO = 2;
-#ifndef GGS_ASMX
-#define GGS_ASMX 0
-#endif
 #ifndef GGS_NOPLAN
 #define GGS_NOPLAN 0      // diagnostic build (tools/probe/traffic_ab.sh): the epilogue reads no plan
 #endif      // s_setprio while culling (1 and 3 measured the same)
@@ -207,10 +204,10 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 // raster -1.0 %, bit-identical).
 #define GGS_RATIO(qy) GGS_EXP2(fminf(__builtin_fmaf((qy), s.c16, 8.0f * bx), 100.0f))
 // The first pair's exponent e = qy (Cc qy + bx) + px for both rows of the pair.
-#if GGS_ASMX
 // Cc broadcast from the low half of the record's (Cc, cx) SGPR pair and bx, px
 // from the low half of VGPR pairs whose high half is never set (op_sel_hi 0): no
-// per-visit broadcast copies of bx and px
+// per-visit broadcast copies of bx and px (LLVM copies a splat of a VGPR into a pair
+// of its own; round 3: raster -0.2 % at 512^2, -0.5 % at 1024^2, bit-identical)
 #define GGS_E1(qy) ({                                                                     \
         f2_t t_, e2_, bxu_, pxu_;                                                         \
         bxu_.x = bx; pxu_.x = px;                                                         \
@@ -218,9 +215,6 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
         asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(t_) : "s"(ccp_), "v"(qy), "v"(bxu_)); \
         asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(e2_) : "v"(qy), "v"(t_), "v"(pxu_)); \
         e2_; })
-#else
-#define GGS_E1(qy) fma2((qy), fma2((f2_t)s.Cc, (qy), bx2), px2)
-#endif
 #define GGS_FOR8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 #define GGS_FOR16P(X) GGS_FOR8(X) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
@@ -346,7 +340,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
             const float px = inx ? __builtin_fmaf(s.A * qx, qx, s.la) : -__builtin_inff();
             const float bx = s.Bc * qx;
-            const f2_t qyv = Ybv - (f2_t)s.cy, bx2 = bx, px2 = px;
+            const f2_t qyv = Ybv - (f2_t)s.cy;
             const int rlo = y0 - ty0 - ph;                     // row test: 4g - rlo in [0, rspan]
             const unsigned rspan = (unsigned)(y1 - y0);
 
