@@ -102,6 +102,7 @@ constexpr int OCC = 3;            // waves per SIMD the register budget is sized
 // -0.5 %; at 1024^2/1024 (33 MB of records) the 8-group rotation is 0.6 % faster)
 constexpr int XCD_SHIFT = 3;
 constexpr int CULL_PRIO = 2;
+
 #ifndef GGS_NOPLAN
 #define GGS_NOPLAN 0      // diagnostic build (tools/probe/traffic_ab.sh): the epilogue reads no plan
 #endif      // s_setprio while culling (1 and 3 measured the same)
@@ -423,11 +424,11 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #undef GGS_FIRST
                 default: __builtin_unreachable();
             }
-            // recurrence walk: f *= r, r *= rho (no exp).  Two pairs per basic
+            // recurrence walk: f *= r, r *= rho (no exp).  Three pairs per basic
             // block (the walk's scalar branches split blocks), so the scheduler
-            // overlaps one pair's blend with the next pair's recurrence
-            // (4 per block measured slower: tools/ablate.py 0.245 vs 0.251 ms).
-            // The last pair (rows below y1 masked) is inlined at both exits of
+            // overlaps one pair's blend with the next pairs' recurrence (round 3:
+            // -0.6 % at 512^2, -0.3 % at 1024^2 vs two; four: a further -0.2 %).
+            // The last pair (rows below y1 masked) is inlined at every exit of
             // each step, so leaving the walk costs no second switch.
 #define GGS_LASTB(k)                                                                    \
     if ((k) < NPK) {                                                                    \
@@ -438,11 +439,16 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         fu_.y = keep_if(bot_.y, fr_.y);                                                 \
         GGS_BLEND(k, fu_);                                                              \
     }
-#define GGS_MID2(k, k1, k2)                                                             \
+#define GGS_MID3(k, k1, k2, k3)                                                         \
     u##k:                                                                               \
-        if (kB > (k2)) {                                                                \
+        if (kB > (k3)) {                                                                \
+            GGS_BLEND_REC(k1) GGS_BLEND_REC(k2) GGS_BLEND_REC(k3)                       \
+            goto u##k3;                                                                 \
+        }                                                                               \
+        if (kB == (k3)) {                                                               \
             GGS_BLEND_REC(k1) GGS_BLEND_REC(k2)                                         \
-            goto u##k2;                                                                 \
+            GGS_LASTB(k3)                                                               \
+            goto done;                                                                  \
         }                                                                               \
         if (kB == (k2)) {                                                               \
             GGS_BLEND_REC(k1)                                                           \
@@ -451,12 +457,20 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         }                                                                               \
         GGS_LASTB(k1)                                                                   \
         goto done;
-            GGS_MID2(0, 1, 2) GGS_MID2(1, 2, 3) GGS_MID2(2, 3, 4) GGS_MID2(3, 4, 5)
-            GGS_MID2(4, 5, 6) GGS_MID2(5, 6, 7) GGS_MID2(6, 7, 8) GGS_MID2(7, 8, 9)
-            GGS_MID2(8, 9, 10) GGS_MID2(9, 10, 11) GGS_MID2(10, 11, 12) GGS_MID2(11, 12, 13)
-            GGS_MID2(12, 13, 14) GGS_MID2(13, 14, 15)
-#undef GGS_MID2
-        u14:                          // pair 15 is the last one there is
+            GGS_MID3(0, 1, 2, 3) GGS_MID3(1, 2, 3, 4) GGS_MID3(2, 3, 4, 5) GGS_MID3(3, 4, 5, 6)
+            GGS_MID3(4, 5, 6, 7) GGS_MID3(5, 6, 7, 8) GGS_MID3(6, 7, 8, 9) GGS_MID3(7, 8, 9, 10)
+            GGS_MID3(8, 9, 10, 11) GGS_MID3(9, 10, 11, 12) GGS_MID3(10, 11, 12, 13)
+            GGS_MID3(11, 12, 13, 14) GGS_MID3(12, 13, 14, 15)
+#undef GGS_MID3
+        u13:                          // pairs 14 and 15 are the last ones there are
+            if (kB == 15) {
+                GGS_BLEND_REC(14)
+                GGS_LASTB(15)
+                goto done;
+            }
+            GGS_LASTB(14)
+            goto done;
+        u14:
             GGS_LASTB(15)
             goto done;
 #undef GGS_LASTB
