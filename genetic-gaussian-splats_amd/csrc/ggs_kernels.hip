@@ -121,6 +121,18 @@ constexpr int CULL_PRIO = 2;
 constexpr float SAT_EPS = 5.9604645e-8f;   // 2^-24
 constexpr int SAT_FIRST = 64, SAT_EVERY = 16;
 constexpr int SAT_MIN_SPLATS = 512;          // launches with fewer splats use the kernel without the check
+// With the check on, the cull hands over at most SAT_BATCH listed splats at a time
+// (not CAP): a 2048²/4096 strip lists ~500, so the blend of the first batch can meet
+// saturation before the cull has scanned the rest of the candidate's splats, and
+// the cut skips that part of the cull too.  Each batch re-exposes the first record
+// fetch, so small batches lose (tools/probe/sat_batch_ab.sh, raster vs CAP: 2048²
+// with 16 candidates 128: +7.2 %, 192: +4.3 %, 256: -4.8 %, 384: -3.0 %; with 2:
+// +8.7, +8.6, +1.3, -3.3 %; 1024²/1024: +0.8, +1.2, 0.0, +0.1 %; SA loop at
+// configs[4], start of a run, 3 alternated runs: 595 it/s -> 601 with 384, 573 with 256).
+#ifndef GGS_SAT_BATCH
+#define GGS_SAT_BATCH 384
+#endif
+constexpr int SAT_BATCH = GGS_SAT_BATCH;
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -295,6 +307,14 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     int* __restrict__ list = &lists[0][0] + wib * CAP;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
+    // every pixel of the strip below SAT_EPS transmittance (wave-uniform)
+    auto saturated = [&]() __attribute__((always_inline)) {
+        float m = 0.0f;
+#define GGS_TMAX(k) if ((k) < NPK) m = fmaxf(m, fmaxf(P_T##k.x, P_T##k.y));
+        GGS_FOR16P(GGS_TMAX)
+#undef GGS_TMAX
+        return !__ballot(m >= SAT_EPS);
+    };
 
     // bounds of the next 64 splats are loaded one chunk ahead (the cull does
     // little work per chunk, so it waits on these loads; two chunks ahead: no gain)
@@ -313,7 +333,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         const uint64_t m = __ballot(hit);
         if (hit) list[cnt + __popcll(m & lt_mask)] = i * (int)sizeof(SplatRec);   // byte offset
         cnt += __popcll(m);
-        if (cnt <= CAP - 64 && base + 64 < N) continue;
+        if (cnt <= (SAT ? SAT_BATCH : CAP) - 64 && base + 64 < N) continue;
         if (cnt == 0) continue;
         __builtin_amdgcn_s_setprio(0);
 #if GGS_TIMING
@@ -515,17 +535,18 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #if GGS_SATURATE
             // (strips reaching past the image keep T = 1 outside it: never cut)
             if (SAT && j >= SAT_FIRST && (j & (SAT_EVERY - 1)) == 0 && sx0 + 15 < W && ty0 + TILE_H <= H) {
-                float m = 0.0f;
-#define GGS_TMAX(k) if ((k) < NPK) m = fmaxf(m, fmaxf(P_T##k.x, P_T##k.y));
-                GGS_FOR16P(GGS_TMAX)
-#undef GGS_TMAX
-                if (!__ballot(m >= SAT_EPS)) {   // skip the rest of the list and of the cull
+                if (saturated()) {   // skip the rest of the list and of the cull
                     base = N;
                     break;
                 }
             }
 #endif
         }
+#if GGS_SATURATE
+        // end of a batch with more splats to cull: stop here if the strip is saturated
+        if (SAT && SAT_BATCH < CAP && base + 64 < N && sx0 + 15 < W && ty0 + TILE_H <= H && saturated())
+            base = N;
+#endif
         cnt = 0;
 #if GGS_TIMING
         { GGS_TMARK(now); t_vis += now - t_mark; t_mark = now; }
