@@ -9,7 +9,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-template <int HEAD>   // HEAD 1: + the visit head (x-terms, 2+1 exps, first blend) per visit
+// BR > 0: + BR scalar control-flow snippets per visit, KIND:
+//   0 s_cmp + s_cbranch_scc1 over one s_nop (TAKEN) or falling through it
+//   1 s_cmp only (SALU, no branch)
+//   2 s_branch (unconditional) over one s_nop
+//   3 s_cbranch_scc1 (taken) on an SCC set once per visit, no compare in between
+//   4 indirect jump: s_getpc_b64 + s_add_u32/s_addc_u32 + s_setpc_b64 over one s_nop
+template <int HEAD, int BR = 0, bool TAKEN = true, int KIND = 0>
 __global__ void __launch_bounds__(64) kern(float* out, int visits, float rho, float cr, float cg, float cb) {
     f2 Rr[16], Gg[16], Bb[16], T[16];
 #pragma unroll
@@ -30,6 +36,21 @@ __global__ void __launch_bounds__(64) kern(float* out, int visits, float rho, fl
             F = (f2){0.5f + v * 1e-9f, 0.4f};
             R = (f2){0.99f, 0.98f};
         }
+        if (KIND == 3 && BR) asm volatile("s_cmp_eq_u32 %0, %0" ::"s"(v) : "scc");
+#pragma unroll
+        for (int b = 0; b < BR; ++b) {
+            if (KIND == 0 && TAKEN)
+                asm volatile("s_cmp_eq_u32 %0, %0\n\ts_cbranch_scc1 1f\n\ts_nop 0\n1:" ::"s"(v) : "scc");
+            if (KIND == 0 && !TAKEN)
+                asm volatile("s_cmp_lg_u32 %0, %0\n\ts_cbranch_scc1 1f\n\ts_nop 0\n1:" ::"s"(v) : "scc");
+            if (KIND == 1) asm volatile("s_cmp_eq_u32 %0, %0" ::"s"(v) : "scc");
+            if (KIND == 2) asm volatile("s_branch 1f\n\ts_nop 0\n1:");
+            if (KIND == 3) asm volatile("s_cbranch_scc1 1f\n\ts_nop 0\n1:");
+            if (KIND == 4) {
+                asm volatile("s_getpc_b64 s[92:93]\n.Lpc%=:\n\ts_add_u32 s92, s92, 1f-.Lpc%=\n\t"
+                             "s_addc_u32 s93, s93, 0\n\ts_setpc_b64 s[92:93]\n\ts_nop 0\n1:" ::: "s92", "s93", "scc");
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             if (k) { F = F * R; R = R * (f2){rho, rho}; }
@@ -46,7 +67,7 @@ __global__ void __launch_bounds__(64) kern(float* out, int visits, float rho, fl
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
-template <int HEAD>
+template <int HEAD, int BR = 0, bool TAKEN = true, int KIND = 0>
 void run(int waves_per_simd) {
     const int blocks = 1024 * waves_per_simd;         // one wave per block, 1024 SIMDs
     const int visits = 2000;
@@ -55,9 +76,9 @@ void run(int waves_per_simd) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    kern<HEAD><<<blocks, 64>>>(out, visits, 0.999f, 0.2f, 0.3f, 0.4f);
+    kern<HEAD, BR, TAKEN, KIND><<<blocks, 64>>>(out, visits, 0.999f, 0.2f, 0.3f, 0.4f);
     (void)hipEventRecord(e0);
-    for (int r = 0; r < 5; ++r) kern<HEAD><<<blocks, 64>>>(out, visits, 0.999f, 0.2f, 0.3f, 0.4f);
+    for (int r = 0; r < 5; ++r) kern<HEAD, BR, TAKEN, KIND><<<blocks, 64>>>(out, visits, 0.999f, 0.2f, 0.3f, 0.4f);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
@@ -65,13 +86,18 @@ void run(int waves_per_simd) {
     ms /= 5;
     const double pk_ops = (double)blocks * visits * (16 * 7 - 2);   // packed ops of the 16 pair steps
     const double cycles = ms * 1e-3 * 2.4e9;                        // nominal clock
-    printf("head=%d waves/SIMD=%d: %.3f ms, %.2f SIMD cycles per pair-step packed op, %.0f ns per visit per wave\n",
-           HEAD, waves_per_simd, ms, cycles * 1024 / pk_ops, ms * 1e6 / visits);
+    static const char* kinds[] = {"cmp+cbranch", "cmp only", "s_branch", "cbranch (scc ready)", "getpc+add+setpc"};
+    printf("head=%d %2d x %-19s%s waves/SIMD=%d: %.3f ms, %.2f SIMD cycles per pair-step packed op, %.0f ns per visit per wave\n",
+           HEAD, BR, BR ? kinds[KIND] : "", BR && KIND == 0 ? (TAKEN ? " taken" : " not-taken") : "", waves_per_simd, ms, cycles * 1024 / pk_ops, ms * 1e6 / visits);
     (void)hipFree(out);
 }
 
 int main() {
     for (int w : {1, 2, 3, 4}) run<0>(w);
     for (int w : {1, 2, 3, 4}) run<1>(w);
+    for (int w : {1, 3}) {
+        run<1, 8, true>(w); run<1, 16, true>(w); run<1, 8, false>(w); run<1, 16, false>(w);
+        run<1, 8, true, 1>(w); run<1, 8, true, 2>(w); run<1, 8, true, 3>(w); run<1, 8, true, 4>(w);
+    }
     return 0;
 }
