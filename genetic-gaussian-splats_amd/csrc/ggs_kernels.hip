@@ -246,7 +246,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
-              const float* __restrict__ clean, const int* __restrict__ live) {
+              const float* __restrict__ clean, const int* __restrict__ live, int CH) {
     __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
 
     const int lane = threadIdx.x & 63;
@@ -264,8 +264,18 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         if ((int64_t)blockIdx.x >= (int64_t)B * nTiles * SPB) return;
     }
     // strip-major grid: B consecutive blocks run one strip (group) for every
-    // candidate; groups go central (heavy) first to shorten the grid's tail
-    const int gi = blockIdx.x / B;
+    // candidate; groups go central (heavy) first to shorten the grid's tail.
+    // Large launches run in candidate chunks of CH (all groups of one chunk, then
+    // the next), so a chunk's records stay cached while its groups run
+    int idx = blockIdx.x, b0 = 0, Bc = B;
+    if (B > CH) {
+        const int per = CH * nTiles * SPB;
+        const int c = idx / per;
+        idx -= c * per;
+        b0 = c * CH;
+        Bc = min(CH, B - b0);
+    }
+    const int gi = idx / Bc;
     const int grp = tile_order ? tile_order[gi] : gi;
     // candidates rotate by one per group: with B % 8 == 0 a fixed b would stay on
     // one XCD (blocks go round-robin to the 8 XCDs) and per-XCD work would be the
@@ -273,7 +283,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     // ... for the large-N instances only every 2^XCD_SHIFT groups: blocks B apart
     // (the next group's block in the same XCD slot) then run the same candidate,
     // whose records stay in that XCD's caches across 8 groups (see XCD_SHIFT)
-    const int b = (int)((blockIdx.x + (gi >> (SAT ? XCD_SHIFT : 0))) % B);
+    const int b = b0 + (int)((idx + (gi >> (SAT ? XCD_SHIFT : 0))) % Bc);
     const int t = grp / SPB;
     const int wv = (grp % SPB) * WPB + wib;           // strip 0..3 of the tile
     const int tx0 = (t % nTX) * TILE;
@@ -834,6 +844,20 @@ int raster_tiles(int H, int W, int* nTX) {
     return tx * ty;
 }
 
+// Candidates per grid chunk: as many as keep CHUNK_BYTES of splat records + cull
+// bounds (80 B per splat) in flight, a multiple of 8 (the XCD count).
+#ifndef GGS_CHUNK_MB
+#define GGS_CHUNK_MB 40
+#endif
+constexpr int64_t CHUNK_BYTES = (int64_t)GGS_CHUNK_MB << 20;
+int raster_chunk(int N) {
+    const int64_t per = (int64_t)(N > 1 ? N : 1) * (int64_t)(sizeof(SplatRec) + sizeof(int4));
+    int64_t ch = CHUNK_BYTES / per;
+    if (ch > (1 << 24)) ch = 1 << 24;
+    ch &= ~int64_t(7);
+    return ch < 8 ? 8 : (int)ch;
+}
+
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty, const float* clean,
@@ -841,9 +865,10 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const i
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
+    const int CH = raster_chunk(N);
 #define GGS_RASTER(M, S)                                                                       \
     hipLaunchKernelGGL((raster_kernel<M, S>), grid, block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
-                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live)
+                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH)
     // the saturation check only where strip lists can grow long (N > SAT_MIN_SPLATS);
     // at the bench's 256 splats the kernel without it is the faster code (+1.6 %)
     const bool sat = N > SAT_MIN_SPLATS;

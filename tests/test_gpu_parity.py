@@ -326,6 +326,28 @@ def test_full_size_bit_reproducible_and_shard_invariant(full_size):
     np.testing.assert_array_equal(a, one)
 
 
+def test_chunked_grid_ragged_last_chunk_equals_small_batches():
+    """Launches whose records exceed the raster's chunk budget run in candidate
+    chunks (raster_chunk: 40 MiB of records + bounds, 80 B per splat → 128
+    candidates at N = 4096).  B = 300 = 128 + 128 + 44 exercises two full chunks
+    and a ragged one; every candidate's fitness and image must equal those of
+    batches that fit one chunk, bit for bit."""
+    H = W = 128
+    N, B = 4096, 300
+    pop = O.synthetic_population(B, N, H, W, seed=77)
+    rng = np.random.default_rng(5)
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
+    whole = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+    parts = np.concatenate([ggs.fitness(pop[i:i + 100], tgt, H, W, 3.0, weight_mask=mask)
+                            for i in range(0, B, 100)])
+    np.testing.assert_array_equal(whole, parts)
+    enc = ggs.encode(pop)
+    imgs = ggs.render(enc, H, W)
+    for i in (0, 127, 128, 255, 256, 299):
+        np.testing.assert_array_equal(imgs[i], ggs.render(enc[i:i + 1], H, W)[0])
+
+
 def test_full_size_sample_vs_oracle(full_size):
     pop, tgt, mask, H, W = full_size
     idx = [0, 63, 127]
