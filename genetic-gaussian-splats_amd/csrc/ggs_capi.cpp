@@ -1095,10 +1095,15 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     s->ocur = onew;
     s->pending = true;
     const float bg[3] = {1.f, 1.f, 1.f};
-    // this rank's contiguous shard of the offspring (all of them on one GPU);
+    // Only offspring[:P - E] survive (algorithm.py:140-141: the next generation is the
+    // E elites + the first P - E offspring, fitnesses likewise); the last E offspring's
+    // fitness is never read (survivors, fused breed, best, curves), so they are bred
+    // (their draws keep the trajectory) but not evaluated.
+    const int Pe = P - (c.elite_k < 1 ? 1 : c.elite_k);
+    // this rank's contiguous shard of the evaluated offspring (all of them on one GPU);
     // every rank bred all P offspring above with the same draws
-    const int per = (P + s->nranks - 1) / s->nranks;
-    const int b0 = std::min(P, s->rank * per), nb = std::min(P, b0 + per) - b0;
+    const int per = (Pe + s->nranks - 1) / s->nranks;
+    const int b0 = std::min(Pe, s->rank * per), nb = std::min(Pe, b0 + per) - b0;
     if (nb > 0) {
         {
             ProfScope ps(s->st, 1);
@@ -1113,7 +1118,7 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
                                     s->nTiles, c.fitness_mode, c.H, c.W, (float*)s->off_fits.p + b0));
         }
     }
-    if (s->comm) {   // one in-place all-gather of the shards' fitness scalars (RCCL, same stream)
+    if (s->comm && per > 0) {   // one in-place all-gather of the shards' fitness scalars (RCCL, same stream)
         float* of = (float*)s->off_fits.p;
         if ((rc = ggs_comm_allgather(s->comm, s->st, of + (int64_t)s->rank * per, of, per, 0, nullptr)))
             return rc;

@@ -425,9 +425,12 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
             off = next_generation(pop, fits, draws, gen, generations, tour_k, cxpb, mutpb,
                                   mut_sigma_max, mut_sigma_min, schedule, H, W,
                                   min_scale_splats, max_scale_splats)
-            off_fits = np.asarray(evaluate(off), np.float32)                 # algorithm.py:123-126
-            elite_idx = np.argsort(fits, kind="stable")[:elite_k_actual]     # algorithm.py:129-131
+            # algorithm.py:123-126 evaluates all offspring, but only off[:keep] survive
+            # (:140-141) and nothing reads the rest's fitness: evaluate the survivors
             keep = pop_size - elite_k_actual
+            off_fits = (np.asarray(evaluate(off[:keep]), np.float32) if keep > 0
+                        else np.zeros(0, np.float32))
+            elite_idx = np.argsort(fits, kind="stable")[:elite_k_actual]     # algorithm.py:129-131
             pop = np.concatenate([pop[elite_idx], off[:keep]], axis=0)
             fits = np.concatenate([fits[elite_idx], off_fits[:keep]], axis=0)  # elites: carried over
             g = int(np.argmin(fits))

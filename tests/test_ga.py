@@ -125,9 +125,12 @@ def test_ga_loop_matches_reference():
     def evaluate(pop):                        # the reference's own fitness values
         k = len(calls)
         ref_call = 0 if k == 0 else 2 * k - 1  # skip the reference's elite re-evaluations
-        np.testing.assert_array_equal(pop, d[f"call{ref_call}__pop"], err_msg=f"call {ref_call}")
+        # offspring: only the P - elite_k that survive are evaluated (the first ones)
+        n = len(pop)
+        assert n == (P if k == 0 else P - max(1, elite_k))
+        np.testing.assert_array_equal(pop, d[f"call{ref_call}__pop"][:n], err_msg=f"call {ref_call}")
         calls.append(ref_call)
-        return d[f"call{ref_call}__fit"].astype(np.float32)
+        return d[f"call{ref_call}__fit"][:n].astype(np.float32)
 
     best, best_fit, st = ga.genetic_approx(
         d["target"], H, W, "cuda", pop_size=P, n_splats=N, generations=G, tour_k=tour_k,

@@ -78,7 +78,7 @@ def test_device_ga_replays_reference_draws():
         k = len(calls)
         ref_call = 0 if k == 0 else 2 * k - 1
         calls.append(ref_call)
-        return d[f"call{ref_call}__fit"].astype(np.float32)
+        return d[f"call{ref_call}__fit"][:len(pop)].astype(np.float32)   # survivors only
 
     rec = RecordingDraws(ReplayDraws(d), float(cxpb))
     ga.genetic_approx(d["target"], H, W, "cuda", pop_size=P, n_splats=N, generations=G,

@@ -71,7 +71,10 @@ if a.backend == "device":
                           "config": {"H": H, "W": W, "splats": a.splats, "pop": a.pop, "gens": a.gens,
                                      "n_gpus": world, "sharded": dist is not None},
                           "ms_per_gen": round(dt / a.gens * 1e3, 4),
-                          "candidate_renders_per_s": round(a.gens * a.pop / dt, 1),
+                          # candidates rendered per generation: the P - elite_k surviving
+                          # offspring (the reference renders all P offspring + the elites again)
+                          "candidate_renders_per_s": round(a.gens * (a.pop - 8) / dt, 1),
+                          "reference_renders_per_gen": a.pop + 8,
                           "best_fit": st["best_fit"]}))
     dga.close()
     if gather is not None:
