@@ -132,6 +132,9 @@ constexpr int SAT_MIN_SPLATS = 512;          // launches with fewer splats use t
 #ifndef GGS_SAT_BATCH
 #define GGS_SAT_BATCH 384
 #endif
+#ifndef GGS_SAT_AHEAD
+#define GGS_SAT_AHEAD 2
+#endif
 constexpr int SAT_BATCH = GGS_SAT_BATCH;
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -326,25 +329,59 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         return !__ballot(m >= SAT_EPS);
     };
 
-    // bounds of the next 64 splats are loaded one chunk ahead (the cull does
-    // little work per chunk, so it waits on these loads; two chunks ahead: no gain)
+    // bounds of the next chunks are loaded ahead (the cull does little work per
+    // chunk, so it waits on these loads): one chunk ahead at the bench's N (4 chunks
+    // per strip; two: no gain there), two for the long saturation-cut culls, in two
+    // registers the cull alternates, two chunks per step (a rotating copy, or a step
+    // that may stop between the two, makes the compiler wait on the newest load)
     auto bounds = [&](int i) { return cbnd[max(i, 0)]; };
-    int4 bbn = bounds(N - 1 - lane);
-    for (int base = 0; base < N; base += 64) {
+#ifndef GGS_CULL_AHEAD
+#define GGS_CULL_AHEAD 2
+#endif
+    constexpr int AHEAD = SAT ? GGS_SAT_AHEAD : GGS_CULL_AHEAD;
+    static_assert(AHEAD >= 1 && AHEAD <= 4, "cull prefetch depth");
+    // issued in chunk order (sched barriers), so each chunk waits vmcnt(AHEAD - 1)
+    int4 bbA = bounds(N - 1 - lane), bbB, bbC, bbD;
+    if constexpr (AHEAD > 1) { __builtin_amdgcn_sched_barrier(0); bbB = bounds(N - 1 - lane - 64); }
+    if constexpr (AHEAD > 2) { __builtin_amdgcn_sched_barrier(0); bbC = bounds(N - 1 - lane - 128); }
+    if constexpr (AHEAD > 3) { __builtin_amdgcn_sched_barrier(0); bbD = bounds(N - 1 - lane - 192); }
+    int base = 0;                     // first splat (from the back) not yet culled
+    // a batch is handed to the blend once it holds more than LIMIT splats; a step
+    // adds at most 64 * AHEAD, so the list (CAP) cannot overflow
+    constexpr int LIMIT = SAT ? SAT_BATCH - 64 : CAP - 64 * AHEAD;
+    static_assert(LIMIT + 64 * AHEAD <= CAP, "cull list capacity");
+    while (base < N) {
         // wave priority: the load-bound cull issues ahead of other waves' blends (+0.4 %)
         __builtin_amdgcn_s_setprio(CULL_PRIO);
         // --- cull 64 splats (descending index = front-to-back) against the strip:
         // one 16-B load per lane (clamped index, no short-circuit: a branchy test
         // splits it into two dependent loads), then a branch-free overlap test
-        const int i = N - 1 - (base + lane);
-        const int4 bb = bbn;                                                  // x0 x1 y0 y1
-        bbn = bounds(i - 64);
-        const bool hit = (i >= 0) & (bb.w >= ty0) & (bb.z <= ty1) & (bb.y >= sx0) & (bb.x <= sx0 + 15);
-        const uint64_t m = __ballot(hit);
-        if (hit) list[cnt + __popcll(m & lt_mask)] = i * (int)sizeof(SplatRec);   // byte offset
-        cnt += __popcll(m);
-        if (cnt <= (SAT ? SAT_BATCH : CAP) - 64 && base + 64 < N) continue;
-        if (cnt == 0) continue;
+#define GGS_CULL_CHUNK(BB)                                                                  \
+        {                                                                                   \
+            const int i = N - 1 - (base + lane);                                            \
+            const int4 bb = BB;                                               /* x0 x1 y0 y1 */ \
+            if (AHEAD == 1) BB = bounds(i - 64);                                            \
+            const bool hit = (i >= 0) & (bb.w >= ty0) & (bb.z <= ty1) & (bb.y >= sx0) & (bb.x <= sx0 + 15); \
+            /* deeper: reload after the test, into the registers just read */              \
+            if (AHEAD > 1) BB = bounds(i - 64 * AHEAD);                                     \
+            const uint64_t m = __ballot(hit);                                               \
+            if (hit) list[cnt + __popcll(m & lt_mask)] = i * (int)sizeof(SplatRec);  /* byte offset */ \
+            cnt += __popcll(m);                                                             \
+            base += 64;                                                                     \
+        }
+        if constexpr (AHEAD == 1) {
+            GGS_CULL_CHUNK(bbA)
+            if (cnt <= LIMIT && base < N) continue;
+        } else {
+            do {                                  // past N: no hits (i < 0), clamped loads
+                GGS_CULL_CHUNK(bbA)
+                GGS_CULL_CHUNK(bbB)
+                if constexpr (AHEAD > 2) GGS_CULL_CHUNK(bbC)
+                if constexpr (AHEAD > 3) GGS_CULL_CHUNK(bbD)
+            } while (cnt <= LIMIT && base < N);
+        }
+#undef GGS_CULL_CHUNK
+        if (cnt == 0) continue;       // (base >= N: the loop ends)
         __builtin_amdgcn_s_setprio(0);
 #if GGS_TIMING
         { GGS_TMARK(now); t_cull += now - t_mark; t_mark = now; n_vis += cnt; }
@@ -554,7 +591,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         }
 #if GGS_SATURATE
         // end of a batch with more splats to cull: stop here if the strip is saturated
-        if (SAT && SAT_BATCH < CAP && base + 64 < N && sx0 + 15 < W && ty0 + TILE_H <= H && saturated())
+        if (SAT && SAT_BATCH < CAP && base < N && sx0 + 15 < W && ty0 + TILE_H <= H && saturated())
             base = N;
 #endif
         cnt = 0;

@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=int, default=2048)
 ap.add_argument("--splats", type=int, default=4096)
 ap.add_argument("--batch", type=int, default=1)
+ap.add_argument("--dump", default="", help="save the raw per-wave records (npz) and print the longest waves")
 a = ap.parse_args()
 H = W = a.size
 rng = np.random.default_rng(0)
@@ -60,3 +61,15 @@ res = {"H": H, "splats": a.splats, "batch": a.batch, "waves": n_waves, "span_us"
        "xcd_live_mid_max": [int(per_xcd_live[mid, x].max()) for x in range(8)],
        "xcd_full_frac_mid": float((per_xcd_live[mid] >= 384).any(axis=1).mean())}
 print(json.dumps(res))
+if a.dump:
+    np.savez(a.dump, buf=buf)
+    top = np.argsort(-dur)[:16]
+    for w in top:     # block, us, cull/visit/epilogue clocks (100 MHz-independent s_memtime), listed, blended
+        print("wave %6d  %6.1f us  cull %8d  visits %8d  epi %6d  listed %4d  blended %4d" %
+              (w, dur[w], buf[w, 2], buf[w, 3], buf[w, 4], buf[w, 6], buf[w, 7]))
+    q = np.argsort(dur)
+    for lo, hi in ((0, 0.5), (0.5, 0.9), (0.9, 0.99), (0.99, 1.0)):
+        sel = q[int(lo * len(q)):int(hi * len(q))]
+        print("duration quantile %.2f-%.2f: mean %.1f us, listed %.0f, blended %.0f, cull share %.3f" %
+              (lo, hi, dur[sel].mean(), buf[sel, 6].mean(), buf[sel, 7].mean(),
+               buf[sel, 2].astype(float).sum() / buf[sel, 2:5].astype(float).sum()))
