@@ -18,10 +18,14 @@ The operators consume the draws with exactly the reference's arithmetic
 reproduce its results bit for bit — tests/test_ga.py replays draws recorded
 from the reference (tests/golden/make_golden_ga.py) to prove it.
 
-One deliberate difference: the reference re-evaluates the elites every
-generation (algorithm.py:134-137).  The evaluator is deterministic (same
-genome → same bits, tests/test_gpu_parity.py), so their fitness is carried
-over instead of recomputed; the returned values are identical.
+Two deliberate differences, both in what is evaluated, not in any result: the
+reference re-evaluates the elites every generation (algorithm.py:134-137); the
+evaluator is deterministic (same genome → same bits, tests/test_gpu_parity.py),
+so their fitness is carried over instead of recomputed.  And it evaluates all
+P offspring (algorithm.py:123-126) although only offspring[:P - elite_k] survive
+(:140-141) and nothing reads the others' fitness; they are bred (their draws keep
+the trajectory) but not evaluated, so an ``evaluate`` hook sees P - elite_k rows
+per generation.  The returned values are identical.
 """
 from __future__ import annotations
 
@@ -364,8 +368,9 @@ def genetic_approx(target_img_uint8, H: int, W: int, device, pop_size: int, n_sp
     """algorithm.py:17-195 → (best individual [N, 9] float32, best fitness).
 
     Extra keyword-only hooks: ``seed`` / ``draws`` (draw source), ``evaluate``
-    (population [P,N,9] → fitness [P]; default: one libggs launch with the
-    importance mask), ``init_population``, ``return_state`` (also return the
+    (population [M,N,9] → fitness [M]: the initial population, then the P -
+    elite_k surviving offspring of each generation; default: one libggs launch
+    with the importance mask), ``init_population``, ``return_state`` (also return the
     final population, fitnesses and curves), ``backend``: "host" (numpy
     operators, one libggs fitness launch per generation), "device" (the whole
     generation on the GPU, ggs/ga_device.py; Philox draws keyed by ``seed``, or
