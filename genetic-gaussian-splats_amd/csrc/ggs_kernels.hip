@@ -119,7 +119,10 @@ constexpr int CULL_PRIO = 2;
 #define GGS_SATURATE 1
 #endif
 constexpr float SAT_EPS = 5.9604645e-8f;   // 2^-24
-constexpr int SAT_FIRST = 64, SAT_EVERY = 16;
+#ifndef GGS_SAT_EVERY
+#define GGS_SAT_EVERY 16
+#endif
+constexpr int SAT_FIRST = 64, SAT_EVERY = GGS_SAT_EVERY;
 constexpr int SAT_MIN_SPLATS = 512;          // launches with fewer splats use the kernel without the check
 // With the check on, the cull hands over at most SAT_BATCH listed splats at a time
 // (not CAP): a 2048²/4096 strip lists ~500, so the blend of the first batch can meet
