@@ -1569,7 +1569,33 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
     double* curves = (double*)s->curves.p;
     GGS_HIP(hipMemcpyAsync(s->sit.p, tab.data(), sizeof(SaItDev) * (size_t)n_its, hipMemcpyHostToDevice, s->st));
     const int64_t pos0 = (int64_t)first_it * tries, end = pos0 + (int64_t)n_its * tries;
-    GGS_HIP(launch_sa_begin(s->st, loop, pos0, end, tries, first_it, s->cap, width));
+    // adaptive width (sa_width_rule): a round's fixed cost in neighbour evaluations,
+    // half the number of candidates whose strip waves fit in the GPU's raster wave
+    // slots (CUs x 4 SIMDs x 3 waves): small canvases add neighbours almost for free
+    // until the chip fills.  2048^2 (2,048 strips): 0.75 — measured at configs[4],
+    // start of a run, a round of 1 neighbour costs 191 us and of 2 297 us (r = 0.81);
+    // 512^2 (128 strips): 12
+    static const double wave_slots = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return 12.0 * (double)cus;
+    }();
+    const double width_r = std::max(0.25, 0.5 * wave_slots / (double)(4 * s->nTiles));
+    // Width of a batch of rounds: the rule's width at the acceptance rate of the
+    // last sync, used by every round of the batch and the size of their mutation
+    // and raster grids — not the session capacity with the width chosen per round
+    // on the device: unused neighbour slots are not free (a lone 2048^2 neighbour in
+    // a 16-slot grid ran 216 us per round instead of 191: the early-exit strip waves
+    // of the other slots stream through the free wave slots beside it).  The
+    // pending round (computed by the previous batch) keeps its width; the
+    // trajectory does not depend on the width.
+    auto batch_width = [&]() {
+        const int w = width > 0 ? width : sa_width_rule(s->h_loop->acc_rate, s->cap, width_r);
+        return std::min(s->cap, std::max(w, 1));
+    };
+    int bw = batch_width(), gcap = bw;
+    GGS_HIP(launch_sa_begin(s->st, loop, pos0, end, tries, first_it, s->cap, width, width_r, bw));
     if ((rc = ensure(s->flags, sizeof(int) * (size_t)(end - pos0), s->st))) return rc;
     GGS_HIP(launch_sa_flags(s->st, pos0, (int)(end - pos0), tries, c.seed, c.mutpb, s->N, (int*)s->flags.p));
     GaParamsDev prm = ga_params(c, first_it, total_iters);   // sigmas replaced per neighbour from sit
@@ -1600,22 +1626,23 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
     auto round = [&]() -> int {
         {
             ProfScope ps(s->st, 0);
-            GGS_HIP(launch_sa_mutate(s->st, loop, sit, prm, c.seed, s->N, s->cap, (int*)s->flags.p,
+            GGS_HIP(launch_sa_mutate(s->st, loop, sit, prm, c.seed, s->N, gcap, (int*)s->flags.p,
                                      (const float*)s->curr.p, (float*)s->nb.p, (float*)s->sizes.p,
                                      (SplatRec*)s->nb_recs.p, (int4*)s->nb_bnds.p, c.H, c.W, c.k_sigma));
         }
         if (s->incremental)
             GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, (const float*)s->nb.p,
-                                 (const SplatRec*)s->cur_recs.p, (const SplatRec*)s->nb_recs.p, s->cap, s->N, c.H,
+                                 (const SplatRec*)s->cur_recs.p, (const SplatRec*)s->nb_recs.p, gcap, s->N, c.H,
                                  c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p, live));
         {
             ProfScope ps(s->st, 1);
-            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->nb_recs.p, (const int4*)s->nb_bnds.p, s->cap, s->N,
+            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->nb_recs.p, (const int4*)s->nb_bnds.p, gcap, s->N,
                                   c.H, c.W, bg, nullptr,
                                   (const float4*)s->plan.p, (float*)s->nb_part.p, (const int*)s->order.p,
                                   s->incremental ? (const unsigned char*)s->dirty.p : nullptr,
                                   (const float*)s->cur_part.p, live));
         }
+        rd.gcap = bw;
         GGS_HIP(launch_sa_accept(s->st, loop, sit, rd));
         return GGS_OK;
     };
@@ -1628,16 +1655,22 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
     // crashed the host thread inside the launch call.
     const uint64_t evaluated0 = s->h_loop->evaluated;
     int64_t remaining = end - pos0;
-    int est = width > 0 ? width : (s->h_loop->acc_rate < 1.0 / s->cap ? s->cap
-                                   : std::max(1, (int)lrint(1.0 / s->h_loop->acc_rate)));
+    int est = gcap;
     for (;;) {
-        const int64_t R = sa_rounds_per_sync(remaining, est);
-        for (int64_t r = 0; r < R; ++r)
+        int64_t R = sa_rounds_per_sync(remaining, est);
+        // the batch width comes from the acceptance rate at this sync: while the
+        // rate has little history (a session's first tries) sync every 2 rounds
+        if (s->h_loop->evaluated < 64) R = std::min<int64_t>(R, 2);
+        for (int64_t r = 0; r < R; ++r) {
             if ((rc = round())) return rc;
+            gcap = bw;                  // after the pending round: every round has width bw
+        }
         GGS_HIP(hipMemcpyAsync(s->h_loop, loop, sizeof(SaLoopDev), hipMemcpyDeviceToHost, s->st));
         GGS_HIP(hipStreamSynchronize(s->st));
         if (s->h_loop->pos >= end) break;
         remaining = end - s->h_loop->pos;
+        bw = batch_width();
+        gcap = std::max(bw, (int)s->h_loop->live);     // the grids also hold the pending round
         est = std::max(1, (int)s->h_loop->live);
     }
     GGS_HIP(hipMemcpyAsync(curves_out, curves, sizeof(double) * 2 * (size_t)n_its, hipMemcpyDeviceToHost, s->st));

@@ -886,9 +886,12 @@ int ga_breed_max_population() { return RANKMAX; }
 // ---------------------------------------------------------------------------
 // Round width: the host loop's rule (ggs/annealing.py) without its iteration
 // boundary — 1/acceptance rate, or the capacity while acceptances are rarer than that.
-__device__ __forceinline__ int sa_width(const SaLoopDev& s) {
-    int w = s.width;
-    if (w <= 0) w = s.acc_rate < 1.0 / s.cap ? s.cap : max(1, (int)rint(1.0 / s.acc_rate));
+// gcap: the width of the batch of rounds the host enqueued (their launch width,
+// <= cap): the host applies sa_width_rule at each sync, so every launched
+// neighbour slot is used (an unused slot's early-exit strip waves are not free)
+__device__ __forceinline__ int sa_width(const SaLoopDev& s, int gcap) {
+    int w = gcap > 0 ? gcap : s.width;
+    if (w <= 0) w = sa_width_rule(s.acc_rate, s.cap, s.width_r);
     w = min(w, s.cap);
     return (int)min((int64_t)w, max(s.end - s.pos, (int64_t)0));
 }
@@ -1057,7 +1060,7 @@ hipError_t launch_sa_mutate(hipStream_t st, const SaLoopDev* sl, const SaItDev* 
 }
 
 __global__ void sa_begin_kernel(SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it, int cap,
-                                int width) {
+                                int width, double width_r, int gcap) {
     SaLoopDev s = *sl;
     s.pos = pos;
     s.end = end;
@@ -1065,9 +1068,10 @@ __global__ void sa_begin_kernel(SaLoopDev* sl, int64_t pos, int64_t end, int tri
     s.first_it = first_it;
     s.cap = cap;
     s.width = width;
+    s.width_r = width_r;
     s.acc_j = -1;
     s.new_best = 0;
-    s.live = sa_width(s);
+    s.live = sa_width(s, gcap);
     *sl = s;
 }
 
@@ -1131,7 +1135,7 @@ sa_accept_kernel(SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, Sa
         }
         s.acc_j = jacc;
         s.new_best = nbest;
-        s.live = sa_width(s);
+        s.live = sa_width(s, r.gcap);
         *sl = s;
         s_j = jacc;
         s_nb = nbest;
@@ -1178,8 +1182,9 @@ sa_accept_kernel(SaLoopDev* __restrict__ sl, const SaItDev* __restrict__ sit, Sa
 }
 
 hipError_t launch_sa_begin(hipStream_t st, SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it,
-                           int cap, int width) {
-    hipLaunchKernelGGL(sa_begin_kernel, dim3(1), dim3(1), 0, st, sl, pos, end, tries, first_it, cap, width);
+                           int cap, int width, double width_r, int gcap) {
+    hipLaunchKernelGGL(sa_begin_kernel, dim3(1), dim3(1), 0, st, sl, pos, end, tries, first_it, cap, width,
+                       width_r, gcap);
     return hipGetLastError();
 }
 

@@ -105,7 +105,25 @@ struct SaLoopDev {
     double best_fit;
     double curr_fit;            // float32 energy of the current state, widened
     uint64_t evaluated, rounds, accepted;
+    double width_r;             // adaptive width: a round's fixed cost / its cost per neighbour
 };
+// Adaptive round width: the w in [1, cap] with the least expected cost per consumed
+// try.  A round of w neighbours costs ~ (r + w) neighbour-evaluations and consumes
+// E(w) = (1 - (1 - p)^w) / p tries at acceptance rate p (it ends at the first
+// acceptance); p -> 0: E = w, so w = cap.  Only the cost depends on w: the
+// trajectory is the same at every width.
+__host__ __device__ inline int sa_width_rule(double p, int cap, double r) {
+    if (cap <= 1) return 1;
+    if (!(p > 1e-9)) return cap;
+    int best_w = 1;
+    double best = 0.0, qw = 1.0;
+    for (int w = 1; w <= cap; ++w) {
+        qw *= 1.0 - p;
+        const double cost = (r + w) * p / (1.0 - qw);
+        if (w == 1 || cost < best) { best = cost; best_w = w; }
+    }
+    return best_w;
+}
 struct SaItDev {                // one iteration of the chunk
     float sig[6];               // build_mut_sigma at this iteration
     float pad_[2];
@@ -130,11 +148,12 @@ struct SaRoundDev {
     SplatRec* cur_recs;         // incremental only (else null)
     const SplatRec* nb_recs;
     float* cur_part;
+    int gcap;                   // the next round's neighbour limit: the batch's launch width
 };
 hipError_t launch_sa_accept(hipStream_t st, SaLoopDev* sl, const SaItDev* sit, const SaRoundDev& r);
-// Start a chunk: pos/end/tries/first_it and the first round's width.
+// Start a chunk: pos/end/tries/first_it and the first round's width (at most gcap).
 hipError_t launch_sa_begin(hipStream_t st, SaLoopDev* sl, int64_t pos, int64_t end, int tries, int first_it,
-                           int cap, int width);
+                           int cap, int width, double width_r, int gcap);
 // Mask-group flags of the chunk's n_tries tries from pos0 (state-independent):
 // tflags [n_tries], zeroed here.
 hipError_t launch_sa_flags(hipStream_t st, int64_t pos0, int n_tries, int tries, uint64_t seed, float mutpb, int N,

@@ -32,6 +32,8 @@ ap.add_argument("--mutpb", type=float, default=0.05)
 ap.add_argument("--dev-iters", type=int, default=200)
 ap.add_argument("--repeat", type=int, default=3)
 ap.add_argument("--temp0", type=float, default=1e-3)
+ap.add_argument("--speculate", type=int, default=0,
+                help="fixed round width for the device variants (0: adaptive, the default)")
 ap.add_argument("--only", default="")
 ap.add_argument("--warm", type=int, default=0,
                 help="start from the best state of a --warm-iteration device run (T0 1e-3), so the "
@@ -74,7 +76,8 @@ for name, spec, backend, inc, loop in variants:
         target, H, W, "cuda", a.splats, a.mutpb, cfg["mut_sigma_max"], cfg["mut_sigma_min"],
         "cosine", 3.0, 0.1, 3.0, 0.7, False, n, a.temp0, "cosine", a.tries, seed=2,
         init_individual=init, evaluate=evaluate if backend == "host" else None, progress=False,
-        return_state=True, speculate=spec, backend=backend, incremental=inc, loop=loop)
+        return_state=True, speculate=(a.speculate or None) if backend == "device" else spec,
+        backend=backend, incremental=inc, loop=loop)
     iters = a.dev_iters if loop == "device" else a.iters
     reps = a.repeat if loop == "device" else 1
     run(2)                                           # warm-up
