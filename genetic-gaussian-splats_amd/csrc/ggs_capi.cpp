@@ -427,7 +427,7 @@ using namespace ggs;
 
 extern "C" {
 
-const char* ggs_version(void) { return "ggs-mi355x 0.1.0 (gfx950)"; }
+const char* ggs_version(void) { return "ggs-mi355x 0.4.0 (gfx950, " GGS_BUILD_KIND " build)"; }
 
 int ggs_init(int32_t max_devices) {
     std::lock_guard<std::mutex> lk(g_mu);

@@ -5,6 +5,22 @@
 
 #include "../../include/ggs.h"
 
+// Diagnostic knobs (per-wave clocks, a plan-less traffic probe that computes the
+// wrong fitness, saturation / cull / chunk overrides) compile only into the probe
+// library (`make probe` -> libggs_probe.so, which ggs/_lib.py refuses unless
+// GGS_PROBE=1), never into libggs.so.
+#if !defined(GGS_PROBE_BUILD) &&                                                         \
+    (defined(GGS_NOPLAN) || defined(GGS_TIMING) || defined(GGS_VTIMING) || defined(GGS_SATURATE) || \
+     defined(GGS_SAT_EVERY) || defined(GGS_SAT_BATCH) || defined(GGS_SAT_AHEAD) ||             \
+     defined(GGS_CULL_AHEAD) || defined(GGS_CHUNK_MB))
+#error "GGS_* diagnostic knobs are for the probe build only: make probe PROBE=\"-D...\""
+#endif
+#ifdef GGS_PROBE_BUILD
+#define GGS_BUILD_KIND "probe"
+#else
+#define GGS_BUILD_KIND "product"
+#endif
+
 namespace ggs {
 
 // One preprocessed splat as the raster kernel consumes it (64 B, HBM + LDS).

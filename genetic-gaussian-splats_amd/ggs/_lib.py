@@ -176,6 +176,12 @@ def _load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # a diagnostic build (csrc/Makefile `make probe`: per-wave clocks, a plan-less
+    # traffic probe with wrong fitness, knob overrides) is never the product
+    kind = (lib.ggs_version() or b"").decode()
+    if "probe build" in kind and os.environ.get("GGS_PROBE") != "1":
+        raise ImportError(f"{LIB_PATH} is a diagnostic probe build ({kind}); set GGS_PROBE=1 to load it "
+                          "for a measurement tool, never for results")
     return lib
 
 

@@ -275,6 +275,32 @@ def test_fitness_vs_oracle_1024_config():
                                                              weight_mask=mask))
 
 
+@pytest.mark.parametrize("N", [512, 513])
+def test_ga_default_config_vs_oracle(N):
+    """The reference's shipped GA run (run_ggs.py:41, config.py:5-11): 512^2 work
+    size, N_SPLATS 512, POP_SIZE 32, ELITE_K 8 -> 24 offspring evaluated per
+    generation.  N = 512 and 513 straddle the raster's instance switch
+    (SAT_MIN_SPLATS in csrc/ggs_kernels.hip: the saturation-checking kernel runs
+    from 513 splats on).  Three of the 24 fitness values vs the oracle (rel 1e-5),
+    a 128x128 centre crop of one image (1e-4 abs), and the launch of 24 equal to
+    the launches of its halves (batch invariance)."""
+    H = W = 512
+    pop = O.synthetic_population(24, N, H, W, seed=50 + N)
+    rng = np.random.default_rng(N)
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0.405, 1.0, (H, W)).astype(np.float32)
+    full = ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=mask)
+    idx = [0, 11, 23]
+    np.testing.assert_allclose(full[idx], O.fitness_many(list(pop[idx]), tgt, H, W, 3.0, weight_mask=mask),
+                               rtol=FIT_RTOL)
+    np.testing.assert_array_equal(full, np.concatenate([ggs.fitness(pop[:12], tgt, H, W, 3.0, weight_mask=mask),
+                                                        ggs.fitness(pop[12:], tgt, H, W, 3.0, weight_mask=mask)]))
+    img = ggs.render(ggs.encode(pop[11:12]), H, W)[0]
+    win = (192, 320, 192, 320)
+    ref = O.render(O.genome_to_renderer_batched(pop[11:12]), H, W, window=win)[0]
+    np.testing.assert_allclose(img[192:320, 192:320], ref, atol=IMG_TOL, rtol=0)
+
+
 def test_render_2048_config_crops_vs_oracle():
     """configs[4] shape (run_sags.py: 2048^2, 4096 splats, one candidate): the GPU
     image on three 96x96 crops (centre, corner, edge) vs the oracle rendering just

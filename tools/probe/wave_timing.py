@@ -1,7 +1,7 @@
 """Per-wave phase timing of the raster kernel (diagnostic build GGS_TIMING=1).
 
-    make -C genetic-gaussian-splats_amd/csrc OUT=../libggs_timing.so BUILD=build_timing EXTRA=-DGGS_TIMING=1
-    GGS_LIB=genetic-gaussian-splats_amd/libggs_timing.so python tools/probe/wave_timing.py
+    make -C genetic-gaussian-splats_amd/csrc probe PROBE=-DGGS_TIMING=1
+    GGS_PROBE=1 GGS_LIB=genetic-gaussian-splats_amd/libggs_probe.so python tools/probe/wave_timing.py
 
 Runs the bench workload (512^2 / 256 splats / B = 128, weighted fitness), then
 reads g_ggs_timing: per wave the realtime start/end (100 MHz), shader clocks

@@ -1,8 +1,8 @@
 """Per-wave timing of one raster launch at any canvas / splat count / batch
 (diagnostic build GGS_TIMING=1), through the host API.
 
-    make -C genetic-gaussian-splats_amd/csrc OUT=../libggs_timing.so BUILD=build_timing EXTRA=-DGGS_TIMING=1
-    GGS_LIB=genetic-gaussian-splats_amd/libggs_timing.so python tools/probe/wave_timing_cfg.py --size 2048 --splats 4096 --batch 1
+    make -C genetic-gaussian-splats_amd/csrc probe PROBE=-DGGS_TIMING=1
+    GGS_PROBE=1 GGS_LIB=genetic-gaussian-splats_amd/libggs_probe.so python tools/probe/wave_timing_cfg.py --size 2048 --splats 4096 --batch 1
 
 Prints the launch span, the wave-duration spread, visits per wave, and the grid
 fill: how long at least 3,072 / 2,048 / 1,024 waves were live."""

@@ -14,11 +14,12 @@ if os.path.exists(stats):
             "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3,
             "pct": float(r["Percentage"])}
 # bench.py's last pass is single-stream with per-launch HIP events (the live
-# avg_launch_ms): average the raster over its dispatches alone (the last STEPS)
-# and over the two-stream timed pass (the first STEPS after warm-up)
+# avg_launch_ms): average the raster over that pass's dispatches alone (the last
+# PROF_STEPS).  Only for the bench (tools/profile.sh sets PROF_BENCH_PASS=1 when it
+# profiles bench.py); other workloads have no such pass and report the trace average.
 trace = os.path.join(root, "trace", "run_kernel_trace.csv")
 steps = int(os.environ.get("PROF_STEPS", "30"))
-if os.path.exists(trace):
+if os.path.exists(trace) and os.environ.get("PROF_BENCH_PASS") == "1":
     rows = [r for r in csv.DictReader(open(trace)) if "raster_kernel" in r.get("Kernel_Name", "")]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]

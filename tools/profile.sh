@@ -20,4 +20,5 @@ run pmc_fetch rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-for
 run pmc_write rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- $BENCH
 run pmc_sq rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc_sq" -o run --output-format csv -- $BENCH
 run pmc_wait rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT -d "$OUT/pmc_wait" -o run --output-format csv -- $BENCH
+case "$BENCH" in *bench.py*) export PROF_BENCH_PASS=1 ;; *) export PROF_BENCH_PASS=0 ;; esac
 python3 tools/prof_summary.py "$OUT" > "$OUT/summary.json" && cat "$OUT/summary.json"
