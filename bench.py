@@ -290,6 +290,158 @@ def spawn_ranks(n: int, argv, python=sys.executable, script=None, gpus_visible=N
     return rc
 
 
+# ---- hang watchdog (N > 1 must fail loudly, never hang) -----------------------------
+WATCHDOG_EXIT = 124
+
+
+def launch_key() -> str:
+    """The key every rank of this launch shares (ggs.parallel.rendezvous_key)."""
+    try:
+        from ggs.parallel import rendezvous_key
+        return rendezvous_key()
+    except ImportError:
+        return os.environ.get("GGS_RDZV_KEY") or f"run-{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}"
+
+
+class Watchdog:
+    """A deadline on every phase of the run (communicator set-up, ramps, timed
+    passes, the extra passes).  The main thread only stores where it is — phase,
+    step, stream, and per communicator the collectives it has ISSUED (an in-stream
+    RCCL gather is issued once its enqueue returned; a host collective once it was
+    entered) — plain attribute stores, nothing on the hot path waits.  A daemon
+    thread writes that state to a heartbeat file beside the RCCL id files every
+    ``period`` s; when a phase outlives its deadline it reads every rank's
+    heartbeat, names the rank(s) that issued the fewest collectives (the rank the
+    others wait for), prints every rank's position to stderr and ends this process
+    with WATCHDOG_EXIT.  No retry, no re-exec.  When no rank is behind, the hang is
+    on the device (a kernel or a collective that never finishes) and the report
+    says so."""
+
+    def __init__(self, rank: int, world: int, key: str, directory=None, period: float = 0.5):
+        import tempfile
+        import threading
+        self.rank, self.world, self.period = rank, world, period
+        self.dir = directory or os.environ.get("GGS_RDZV_DIR") or tempfile.gettempdir()
+        self.key = key
+        self.phase, self.step, self.stream = "start", -1, -1
+        self.issued = {}                              # communicator -> collectives issued
+        self.last_ticket = None
+        self.deadline = None
+        self.budget = 0.0
+        self.t_arm = time.monotonic()
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="bench-watchdog", daemon=True)
+        self._thread.start()
+
+    def path(self, r: int) -> str:
+        return os.path.join(self.dir, f"ggs-hb-{self.key}-r{r}.json")
+
+    # ---- main thread -------------------------------------------------------------------
+    def arm(self, phase: str, seconds: float) -> None:
+        self.phase, self.budget, self.t_arm = phase, float(seconds), time.monotonic()
+        self.deadline = self.t_arm + float(seconds)
+
+    def disarm(self) -> None:
+        self.deadline = None
+
+    def collective(self, comm: int, ticket=None) -> None:
+        self.issued[comm] = self.issued.get(comm, 0) + 1
+        if ticket is not None:
+            self.last_ticket = ticket
+
+    def close(self) -> None:
+        self._stop.set()
+        self._thread.join(2 * self.period + 1)
+        try:
+            os.unlink(self.path(self.rank))
+        except OSError:
+            pass
+
+    # ---- watchdog thread ---------------------------------------------------------------
+    def state(self) -> dict:
+        return {"rank": self.rank, "phase": self.phase, "step": self.step, "stream": self.stream,
+                "issued": {str(k): v for k, v in sorted(self.issued.items())},
+                "issued_total": sum(self.issued.values()), "last_ticket": self.last_ticket,
+                "in_phase_s": round(time.monotonic() - self.t_arm, 3), "wall": time.time()}
+
+    def _write(self) -> None:
+        tmp = f"{self.path(self.rank)}.{os.getpid()}.tmp"
+        try:
+            with open(tmp, "w") as f:
+                json.dump(self.state(), f)
+            os.replace(tmp, self.path(self.rank))
+        except OSError:
+            pass
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.period):
+            self._write()
+            d = self.deadline
+            if d is not None and time.monotonic() > d:
+                self._expire()
+
+    def peers(self) -> dict:
+        out = {}
+        for r in range(self.world):
+            try:
+                with open(self.path(r)) as f:
+                    out[r] = json.load(f)
+            except (OSError, ValueError):
+                out[r] = None
+        return out
+
+    @staticmethod
+    def stalled(peers: dict, now: float, stale_s: float):
+        """(ranks named as stalled, reason).  A rank whose heartbeat is missing or
+        older than ``stale_s`` is frozen or gone; otherwise the ranks that issued
+        the fewest collectives hold everyone else up; all equal: a device hang."""
+        gone = [r for r, s in peers.items() if s is None or now - s["wall"] > stale_s]
+        if gone:
+            return gone, "no heartbeat (process frozen or gone)"
+        counts = {r: s["issued_total"] for r, s in peers.items()}
+        lo, hi = min(counts.values()), max(counts.values())
+        if lo < hi:
+            return sorted(r for r, c in counts.items() if c == lo), \
+                f"issued {lo} collectives while the others issued up to {hi}"
+        return [], f"every rank issued the same {lo} collectives: the hang is on the device"
+
+    def _expire(self) -> None:
+        self._write()
+        time.sleep(min(self.period, 0.2))
+        peers = self.peers()
+        bad, why = self.stalled(peers, time.time(), stale_s=10 * self.period + 2)
+        s = self.state()
+        lines = [f"bench.py watchdog: rank {self.rank}: phase '{self.phase}' exceeded its "
+                 f"{self.budget:.1f} s deadline (step {s['step']}, stream {s['stream']}, "
+                 f"collectives issued per communicator {s['issued']}, last gather ticket "
+                 f"{s['last_ticket']})",
+                 f"bench.py watchdog: stalled rank(s): {bad if bad else 'none identified'} — {why}"]
+        for r, p in sorted(peers.items()):
+            lines.append(f"bench.py watchdog:   rank {r}: " + ("no heartbeat" if p is None else
+                         f"phase '{p['phase']}' step {p['step']} stream {p['stream']} issued {p['issued']} "
+                         f"last ticket {p['last_ticket']} ({p['in_phase_s']:.1f} s in phase)"))
+        sys.stderr.write("\n".join(lines) + "\n")
+        sys.stderr.flush()
+        os._exit(WATCHDOG_EXIT)
+
+
+def stream_accounting(n_streams: int, distributed: bool, gather: str, hw_queues: int) -> dict:
+    """The HIP streams this process holds against GPU_MAX_HW_QUEUES.  Streams
+    that carry collectives: the compute streams (in-stream gathers) or, with
+    "rccl-overlap", each communicator's own stream; plus communicator 0's own
+    stream, which runs the host-side barrier / max-over-ranks gathers.  RCCL's
+    internal streams (about two per communicator) carry no gather kernel of ours.
+    Two collective-carrying streams on one hardware queue would serialise one
+    rank's gathers behind another's, so more of them than queues is refused."""
+    comms = n_streams if distributed and gather.startswith("rccl") else 0
+    own = 0 if not comms else (comms if gather == "rccl-overlap" else 1)
+    carrying = 0 if not comms else (own if gather == "rccl-overlap" else n_streams + own)
+    return {"compute_streams": n_streams, "communicators": comms, "communicator_streams": own,
+            "rccl_internal_streams_est": 2 * comms, "total_est": n_streams + own + 2 * comms,
+            "collective_streams": carrying, "gpu_max_hw_queues": hw_queues,
+            "ok": carrying <= hw_queues}
+
+
 # ---- the benchmark ---------------------------------------------------------------------
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
@@ -309,6 +461,11 @@ def parse_args(argv=None):
                          "and are not the BASELINE workload)")
     ap.add_argument("--extras", type=int, default=1,
                     help="0: headline pass only (profiling runs)")
+    ap.add_argument("--watchdog-init-s", type=float, default=300.0,
+                    help="deadline of the communicator set-up and the first barrier")
+    ap.add_argument("--watchdog-floor-s", type=float, default=30.0,
+                    help="every later phase's deadline: this floor + 20x its expected time from the "
+                         "step time measured locally in the ramp")
     return ap.parse_args(argv)
 
 
@@ -348,9 +505,18 @@ def run(args, world, rank, local_rank, distributed):
         cpu = cpu_baseline(tgt_h, mask_h)
 
     # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the
-    # gathers' RCCL streams take queues too, so ask for 8 before HIP starts
+    # gathers' RCCL streams take queues too, so ask for 8 before HIP starts, and
+    # refuse a layout with more collective-carrying streams than queues
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
         os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    acct = stream_accounting(args.streams, distributed, GATHER, int(os.environ["GPU_MAX_HW_QUEUES"]))
+    print(f"bench.py: rank {rank}: streams {acct}", file=sys.stderr, flush=True)
+    if not acct["ok"]:
+        raise SystemExit(f"bench.py: {acct['collective_streams']} streams would carry collectives but "
+                         f"GPU_MAX_HW_QUEUES={acct['gpu_max_hw_queues']}: two of them could share a "
+                         f"hardware queue and serialise one rank's gathers behind another's")
+    wd = Watchdog(rank, world, launch_key())
+    wd.arm("set-up (device, target plan, communicators, first barrier)", args.watchdog_init_s)
     os.environ.setdefault("GGS_HIP_RUNTIME", "system")   # no torch in this process: /opt/rocm's HIP
     import ggs
     from ggs import hip
@@ -390,14 +556,17 @@ def run(args, world, rank, local_rank, distributed):
         works[j] = None
 
     def step(i, ns, gather=True):
-        g, j, st = pops[i % N_POPS], i % RING, sts[i % ns]
+        g, j, k = pops[i % N_POPS], i % RING, i % ns
+        st = sts[k]
+        wd.step, wd.stream = i, k
         join(j)
         plan.fitness_device(st, g.ptr, POP, N_SPLATS, 9, K_SIGMA, outs[j].ptr)
         if comms is None or not gather:
             return
         # RCCL: fitness scalars to every rank
-        works[j] = (i % ns, comms[i % ns].allgather(st, outs[j].ptr, gathered[j].ptr, POP,
-                                                    overlap=GATHER == "rccl-overlap"))
+        works[j] = (k, comms[k].allgather(st, outs[j].ptr, gathered[j].ptr, POP,
+                                          overlap=GATHER == "rccl-overlap"))
+        wd.collective(k, works[j][1])
 
     def barrier():
         for j in range(RING):
@@ -405,13 +574,23 @@ def run(args, world, rank, local_rank, distributed):
         for s in streams:
             s.synchronize()
         if comms is not None:
+            wd.collective(0)
             comms[0].barrier()
         hip.synchronize()
+
+    # every later phase's deadline: the floor + 20x its expected time at the step
+    # time this rank measured alone (the first ramp batch: no collectives)
+    t_step = [None]
+
+    def arm(phase, n_steps=0, extra_s=0.0):
+        est = (t_step[0] or 0.0) * n_steps + extra_s
+        wd.arm(phase, args.watchdog_floor_s + 20.0 * est)
 
     # Clock ramp before any measurement: the GPU raises its clocks over tens of ms
     # of load, so run the evaluation untimed for --ramp-ms first (no gathers:
     # ranks may run different numbers of these steps).
     def ramp(ms, ns):
+        arm(f"ramp ({ms:.0f} ms, {ns} stream(s))", extra_s=ms * 1e-3)
         t_ramp, i = time.perf_counter(), 0
         while (time.perf_counter() - t_ramp) * 1e3 < ms:
             for _ in range(50):
@@ -419,12 +598,15 @@ def run(args, world, rank, local_rank, distributed):
                 i += 1
             for s in streams:
                 s.synchronize()
+            if t_step[0] is None:
+                t_step[0] = (time.perf_counter() - t_ramp) / 50
         barrier()
 
     def max_over_ranks(vals):
         v = np.asarray(vals, np.float64)
         if comms is None:
             return v
+        wd.collective(0)
         return comms[0].allgather_host(v.astype(np.float32)).astype(np.float64).max(0)
 
     def timed(ns):
@@ -432,11 +614,13 @@ def run(args, world, rank, local_rank, distributed):
         barrier + synchronize, until --min-time seconds were measured (the same
         number of passes on every rank).  Returns (median pass seconds after the
         max over ranks per pass, passes, host enqueue seconds of the first pass)."""
+        arm(f"warm-up ({args.warmup} steps, {ns} stream(s))", args.warmup)
         for i in range(args.warmup):
             step(i, ns)
         barrier()
 
         def one_pass():
+            arm(f"timed pass ({args.steps} steps, {ns} stream(s))", args.steps)
             t0 = time.perf_counter()
             for i in range(args.steps):
                 step(i, ns)
@@ -472,6 +656,7 @@ def run(args, world, rank, local_rank, distributed):
         # + the D2H of the B fitness scalars each step (fitness.py:42 .cpu()) and a host sync
         ramp(args.ramp_ms / 3, 1)
         host_out = np.empty(POP, np.float32)
+        arm("readback passes", extra_s=args.min_time)
         t0 = time.perf_counter()
         n_rb = 0
         while time.perf_counter() - t0 < args.min_time:
@@ -489,6 +674,7 @@ def run(args, world, rank, local_rank, distributed):
         # (ggs_fitness_device) rebuilds it on every call: its one-stream rate, and the
         # plan build alone (host-timed around a synchronised ggs_plan_create).
         ramp(args.ramp_ms / 3, 1)
+        arm("unplanned device-API passes", extra_s=args.min_time)
         t0, n_u = time.perf_counter(), 0
         while time.perf_counter() - t0 < args.min_time:
             for i in range(args.steps):
@@ -516,6 +702,7 @@ def run(args, world, rank, local_rank, distributed):
 
         # per-kernel device time (HIP events on the launch stream) over a single-stream
         # pass (kernels alone, not sharing the chip with another stream's)
+        arm("per-kernel event pass", args.steps)
         ggs.profile_reset()
         ggs.profile_enable(True)
         for i in range(args.steps):
@@ -523,6 +710,7 @@ def run(args, world, rank, local_rank, distributed):
         barrier()
         ggs.profile_enable(False)
         kern = {k: ggs.profile_read(k) for k in ("prep", "raster", "finalize")}
+    wd.disarm()
     if distributed:
         assert shard_ok, "fitness all-gather returned a different shard"
 
@@ -561,10 +749,16 @@ def run(args, world, rank, local_rank, distributed):
         profiled = prof_cfg is not None
         traffic, traffic_src = pmc_traffic(prof_cfg) if profiled else (None, None)
         valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
-        roof = {"bound": "hbm", "kernel": "raster_kernel<1, false>" if N_SPLATS <= 512 else
+        busy = pmc_valu_busy(prof_cfg) if profiled else None
+        _, busy_src = _summary(prof_cfg) if profiled else (None, None)
+        # The raster is bound by the VALU: `bound` names
+        # that roof.  achieved / peak / frac are the HBM figures the contract defines
+        # (algorithmic bytes per launch / HIP-event launch time vs 8 TB/s, frac_roof);
+        # the VALU's executed-work fraction is binding_frac (PMC busy).
+        roof = {"bound": "valu", "kernel": "raster_kernel<1, false>" if N_SPLATS <= 512 else
                 "raster_kernel<1, true>",
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "frac_roof": "hbm",
                 "traffic": None if traffic is None else round(traffic),
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": step_bytes,
@@ -574,21 +768,25 @@ def run(args, world, rank, local_rank, distributed):
                           "--streams 1)",
                 "rocprof_trace_avg_ms": (None if not profiled or pmc_trace_avg_us(prof_cfg) is None
                                          else round(pmc_trace_avg_us(prof_cfg) / 1e3, 5)),
-                # the roof that binds: the VALU; frac above is
-                # the HBM fraction the contract asks for, not the limiter
                 "binding": "valu",
-                "binding_busy_pmc": pmc_valu_busy(prof_cfg) if profiled else None,
+                "binding_frac": busy,
                 "step_effective": {"regime": f"headline, {args.streams} streams (overlapping batches)",
                                    "achieved": round(step_bytes / (ms_step * 1e-3) / 1e9, 2),
                                    "frac": round(step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                                    "ms_per_step": round(ms_step, 5)},
                 "note": "VALU/transcendental-bound path (SURVEY.md §8d): see 'valu'"}
-        valu = {"achieved": round(valu_tflops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
-                "flop_per_aabb_pair": FLOP_PER_PAIR, "aabb_pairs_per_candidate": pairs_per_cand,
-                "accounting": "reference-equivalent work: 24 FLOP per AABB pair (SURVEY.md §8d); "
-                              "the row recurrence executes fewer, so frac can exceed 1",
-                "busy_pmc": pmc_valu_busy(prof_cfg) if profiled else None}
+        valu = {"frac": busy,
+                "frac_definition": "executed VALU issue of the raster kernel: SQ_ACTIVE_INST_VALU x 4 / "
+                                   "(GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), committed rocprofv3 PMC "
+                                   "profile of this launch shape",
+                "frac_source": busy_src,
+                "reference_equivalent": {
+                    "tflops": round(valu_tflops, 3), "fp32_peak_tflops": VALU_PEAK_TFLOPS,
+                    "ratio_to_peak": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
+                    "flop_per_aabb_pair": FLOP_PER_PAIR, "aabb_pairs_per_candidate": pairs_per_cand,
+                    "note": "24 FLOP per AABB pair the reference's per-pixel loop would execute "
+                            "(SURVEY.md §8d); the row recurrence executes fewer, so this ratio can "
+                            "exceed 1 and is not a roofline fraction"}}
     if rank == 0:
         line = {
             "metric": METRIC if headline else
@@ -596,6 +794,11 @@ def run(args, world, rank, local_rank, distributed):
             + (f" split over {world} GPU(s)" if scaling == "strong" else f" per GPU x {world}"),
             "value": round(value, 1),
             "unit": "candidate renders/s",
+            "value_semantics": (f"throughput of independent populations alternating over {args.streams} "
+                                "HIP streams (one batch's grid tail overlaps the next batch); "
+                                "value_one_stream is the rate a generation-by-generation caller "
+                                "(algorithm.py:123-141: the next generation needs this one's fitness) "
+                                "gets, value_with_readback adds the per-step D2H of the fitness scalars"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -632,6 +835,7 @@ def run(args, world, rank, local_rank, distributed):
         print(json.dumps(line), flush=True)
     for c in comms or ():
         c.close()
+    wd.close()
 
 
 def _mapped(name):

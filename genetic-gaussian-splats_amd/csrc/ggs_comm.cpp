@@ -118,13 +118,23 @@ int ensure_scratch(Comm* c, int64_t floats) {
     return GGS_OK;
 }
 
-// Finish a freshly made communicator (its side stream and events).
-int comm_setup(Comm* c) {
-    hipError_t he = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
+// The communicator's own stream and its events, made at the first call that
+// needs them (an overlapped gather or a host-side collective): a communicator
+// used only for in-stream gathers holds no stream of its own, so it takes no
+// hardware queue (bench.py counts the streams that carry collectives against
+// GPU_MAX_HW_QUEUES).  Called with c->mu held and c->dev current.
+int ensure_side(Comm* c) {
+    if (c->side) return GGS_OK;
+    hipStream_t s = nullptr;
+    hipError_t he = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (he == hipSuccess && !c->ready) he = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
     for (int i = 0; he == hipSuccess && i < kTickets; ++i)
-        he = hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming);
-    if (he != hipSuccess) return cfail(GGS_EHIP, "communicator set-up: %s", hipGetErrorString(he));
+        if (!c->done[i]) he = hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming);
+    if (he != hipSuccess) {
+        if (s) (void)hipStreamDestroy(s);
+        return cfail(GGS_EHIP, "communicator stream set-up: %s", hipGetErrorString(he));
+    }
+    c->side = s;
     return GGS_OK;
 }
 
@@ -178,7 +188,6 @@ int ggs_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t*
     int rc = GGS_OK;
     ncclResult_t nr = R.comm_init_rank(&c->nc, nranks, u, rank);
     if (nr != ncclSuccess) rc = cfail(GGS_EHIP, "ncclCommInitRank: %s", R.error_string(nr));
-    if (!rc) rc = comm_setup(c);
     if (rc) {
         ggs_comm_destroy(c);
         return rc;
@@ -213,6 +222,7 @@ int ggs_comm_allgather(void* comm, void* stream, const float* d_send, float* d_r
     }
     // overlap: the gather waits for the work already on `stream` (the fitness
     // kernels that wrote d_send), then runs on the side stream
+    if (int rc = ensure_side(c)) return rc;
     GGS_HIPC(hipEventRecord(c->ready, st));
     GGS_HIPC(hipStreamWaitEvent(c->side, c->ready, 0));
     GGS_NCCL(R.all_gather(d_send, d_recv, (size_t)count, ncclFloat32, c->nc, c->side));
@@ -276,7 +286,6 @@ int ggs_comm_init_local(int32_t n, const int32_t* devices, void** comms) {
         ncclResult_t nr = R.comm_init_all(ncs.data(), n, devices);
         if (nr != ncclSuccess) return cfail(GGS_EHIP, "ncclCommInitAll: %s", R.error_string(nr));
     }
-    int rc = GGS_OK;
     for (int i = 0; i < n; ++i) {
         Comm* c = new Comm;
         c->dev = devices[i];
@@ -284,14 +293,6 @@ int ggs_comm_init_local(int32_t n, const int32_t* devices, void** comms) {
         c->rank = i;
         c->nc = ncs[i];
         comms[i] = c;
-        if (!rc) {
-            DevScope ds(c->dev);
-            rc = comm_setup(c);
-        }
-    }
-    if (rc) {
-        for (int i = 0; i < n; ++i) { ggs_comm_destroy(comms[i]); comms[i] = nullptr; }
-        return rc;
     }
     return GGS_OK;
 }
@@ -305,7 +306,8 @@ int ggs_comm_allgather_host(void* comm, const float* send, float* recv, int64_t 
     std::lock_guard<std::mutex> lk(c->mu);
     DevScope ds(c->dev);
     const int64_t cnt = std::max<int64_t>(count, 1);    // a zero-length call still synchronises the ranks
-    int rc = ensure_scratch(c, cnt * (1 + c->nranks));
+    int rc = ensure_side(c);
+    if (!rc) rc = ensure_scratch(c, cnt * (1 + c->nranks));
     if (rc) return rc;
     float* d_send = c->scratch;
     float* d_recv = c->scratch + cnt;

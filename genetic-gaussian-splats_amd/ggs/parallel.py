@@ -152,12 +152,15 @@ def rendezvous_key() -> str:
     """Names one launch of one job on this node: every rank of it computes the
     same key.  ``GGS_RDZV_KEY`` overrides; otherwise the launcher's parent pid
     (torchrun's agent or bench.py's spawner starts every local rank) with
-    MASTER_PORT and the run id."""
+    MASTER_PORT, the run id and the elastic restart count — torchrun's agent
+    survives a ``--max-restarts`` restart with the same pid, port and run id, so
+    without the count a restarted rank could read the id file the crashed
+    attempt left (newer than the agent, so ``launch_time`` does not reject it)."""
     k = os.environ.get("GGS_RDZV_KEY")
     if k:
         return k
     return "-".join([os.environ.get("TORCHELASTIC_RUN_ID", "run"), os.environ.get("MASTER_PORT", "0"),
-                     str(os.getppid())])
+                     str(os.getppid()), "a" + os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")])
 
 
 def file_rendezvous(rank: int, world: int, make_id, key: Optional[str] = None,
@@ -166,8 +169,10 @@ def file_rendezvous(rank: int, world: int, make_id, key: Optional[str] = None,
     without a process group: rank 0 writes it atomically (tmp + rename) to a file
     named by ``key`` and a per-process sequence number (the n-th communicator
     every rank makes); the others poll for it and accept only a file written after
-    the launch began (``launch_time``), so an id left behind by a launch that
-    crashed before rank 0 could remove it is never read.  Rank 0 removes the file
+    the launch began (``launch_time``), so an id left behind by an earlier launch
+    that crashed before rank 0 could remove it is never read (an elastic restart
+    under the same agent is told apart by the restart count in
+    ``rendezvous_key``, not by the file's age).  Rank 0 removes the file
     once the communicator exists (all ranks have read it: RCCL's init is
     collective).  Single node only — the scope of north_star's 8-GPU sharding."""
     seq = _RDZV_SEQ[0]

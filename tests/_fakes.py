@@ -8,7 +8,13 @@
   rank checks that it received rank 0's bytes.  Each message carries
   (communicator sequence number, call number, kind), so two ranks that issue
   their collectives in a different order or a different number of times fail
-  loudly instead of pairing the wrong calls.
+  loudly instead of pairing the wrong calls.  Like an in-stream RCCL gather,
+  ``allgather`` only posts this rank's part and returns; the peers' parts are
+  received when a host collective (``barrier`` / ``allgather_host``) or a full
+  in-flight window drains the posted calls of every communicator in issue order
+  (they share the pipes).  ``stall=(rank, n)`` makes
+  that rank block forever in its n-th gather before posting it (a rank that
+  never issues a collective the others wait on).
 * ``install_fake_gpu``: ``ggs`` / ``ggs.hip`` modules whose device memory is a
   registry of numpy arrays, so ``bench.run()`` executes its whole distributed
   control flow (rendezvous, ramps, timed passes, max over ranks, shard check,
@@ -60,13 +66,19 @@ class PipeMesh:
 class PipeComm:
     _seq = itertools.count()              # n-th communicator this process made
 
-    def __init__(self, mesh: PipeMesh, rank: int, world: int, log=None, corrupt=False, key=None):
+    WINDOW = 8                            # posted gathers before a forced drain
+    _pending = []                         # posted, not yet received (issue order, all communicators)
+    _gathers = itertools.count()          # gathers this process entered (all communicators)
+
+    def __init__(self, mesh: PipeMesh, rank: int, world: int, log=None, corrupt=False, key=None,
+                 stall=None):
         file_rendezvous = real_parallel().file_rendezvous
         self.mesh, self.rank, self.world, self.log = mesh, rank, world, log
-        self.corrupt = corrupt
+        self.corrupt, self.stall = corrupt, stall
         self.cid = next(PipeComm._seq)
         self.calls = 0
         self.tickets = {}
+        self.pending = PipeComm._pending      # one queue: every communicator shares the pipes
         idb = file_rendezvous(rank, world, lambda: os.urandom(128), key)
         ids = self._exchange("id", np.frombuffer(idb, np.uint8).copy())
         assert all(bytes(x) == bytes(ids[0]) for x in ids), "ranks received different communicator ids"
@@ -74,39 +86,57 @@ class PipeComm:
         if log is not None:
             log.setdefault("comms", []).append({"cid": self.cid, "id": self.id.hex()[:16]})
 
-    def _exchange(self, kind: str, payload: np.ndarray):
-        """Every rank's payload, in rank order (pairwise, lower rank sends first)."""
+    def _post(self, kind: str, payload: np.ndarray, done) -> None:
+        """Send this rank's payload to every peer now; ``done(parts)`` runs when
+        the call is drained."""
         tag = (self.cid, self.calls, kind)
         self.calls += 1
-        out = [None] * self.world
-        out[self.rank] = payload
         for q in range(self.world):
-            if q == self.rank:
-                continue
-            c = self.mesh.peer(self.rank, q)
-            msgs = []
-            if self.rank < q:
-                c.send((tag, payload))
-            if not c.poll(TIMEOUT_S):
-                raise TimeoutError(f"rank {self.rank}: no {kind} from rank {q} (call {tag})")
-            msgs.append(c.recv())
-            if self.rank > q:
-                c.send((tag, payload))
-            rtag, data = msgs[0]
-            if rtag != tag:
-                raise AssertionError(f"rank {self.rank} issued {tag} but rank {q} issued {rtag}")
-            out[q] = data
-        return out
+            if q != self.rank:
+                self.mesh.peer(self.rank, q).send((tag, payload))
+        self.pending.append((tag, payload, done))
+
+    def _drain(self) -> None:
+        """Receive every posted call's parts from the peers, in issue order."""
+        while self.pending:
+            tag, payload, done = self.pending.pop(0)
+            out = [None] * self.world
+            out[self.rank] = payload
+            for q in range(self.world):
+                if q == self.rank:
+                    continue
+                c = self.mesh.peer(self.rank, q)
+                if not c.poll(TIMEOUT_S):
+                    raise TimeoutError(f"rank {self.rank}: no {tag[2]} from rank {q} (call {tag})")
+                rtag, data = c.recv()
+                if rtag != tag:
+                    raise AssertionError(f"rank {self.rank} issued {tag} but rank {q} issued {rtag}")
+                out[q] = data
+            done(out)
+
+    def _exchange(self, kind: str, payload: np.ndarray):
+        """Every rank's payload, in rank order (a blocking call: drains first)."""
+        box = []
+        self._post(kind, payload, box.append)
+        self._drain()
+        return box[0]
 
     # ---- the RcclGather interface --------------------------------------------------
     def allgather(self, stream, d_send, d_recv, count, overlap=False):
+        if self.stall is not None and self.stall[0] == self.rank and next(PipeComm._gathers) == self.stall[1]:
+            import time
+            time.sleep(3600)                          # never issues this gather
         send = MEM[d_send].reshape(-1)[:count].copy()
-        parts = self._exchange("gather", send)
-        recv = MEM[d_recv].reshape(-1)
-        for r, p in enumerate(parts):
-            recv[r * count:(r + 1) * count] = p
-        if self.corrupt:
-            recv[self.rank * count] += 1.0
+
+        def done(parts):
+            recv = MEM[d_recv].reshape(-1)
+            for r, p in enumerate(parts):
+                recv[r * count:(r + 1) * count] = p
+            if self.corrupt:
+                recv[self.rank * count] += 1.0
+        self._post("gather", send, done)
+        if len(self.pending) >= self.WINDOW:
+            self._drain()
         if self.log is not None:
             g = self.log.setdefault("gathers", {})
             g[str(self.cid)] = g.get(str(self.cid), 0) + 1
@@ -119,6 +149,7 @@ class PipeComm:
 
     def wait(self, stream, ticket):
         if ticket >= 0:
+            self._drain()
             assert self.tickets.pop(ticket), "wait on an unknown ticket"
 
     def allgather_host(self, values):
@@ -164,7 +195,7 @@ class _Stream:
         pass
 
 
-def install_fake_gpu(mesh, rank, world, log, slow_rank=None, corrupt=False):
+def install_fake_gpu(mesh, rank, world, log, slow_rank=None, corrupt=False, stall=None):
     """Put stand-in ``ggs`` and ``ggs.hip`` modules in sys.modules."""
     import time
 
@@ -201,7 +232,9 @@ def install_fake_gpu(mesh, rank, world, log, slow_rank=None, corrupt=False):
     def fitness_device(dev, st, d_gen, B, N, Cc, d_t, d_m, mode, beta, H, W, k, d_out):
         TargetPlan(dev, st, d_t, d_m, mode, beta, H, W).fitness_device(st, d_gen, B, N, Cc, k, d_out)
     ggs.fitness_device = fitness_device
-    ggs.RcclGather = lambda local_rank: PipeComm(mesh, rank, world, log, corrupt)
+    ggs.fitness = lambda G, tgt, H, W, k, weight_mask=None, device=0: \
+        np.asarray(G, np.float32).reshape(len(G), -1).sum(1, dtype=np.float32)
+    ggs.RcclGather = lambda local_rank: PipeComm(mesh, rank, world, log, corrupt, stall=stall)
     ggs.profile_reset = prof.clear
     ggs.profile_enable = lambda on: None
     ggs.profile_read = lambda k: (0.1, 1)
@@ -212,5 +245,6 @@ def install_fake_gpu(mesh, rank, world, log, slow_rank=None, corrupt=False):
         z = np.zeros(n, np.int32)
         return {"x0": z, "x1": z + 3, "y0": z, "y1": z + 3}
     ggs.preprocess = preprocess
-    sys.modules["ggs"], sys.modules["ggs.hip"] = ggs, hip
+    ggs.parallel = real_parallel()          # rendezvous_key for the heartbeat files
+    sys.modules["ggs"], sys.modules["ggs.hip"], sys.modules["ggs.parallel"] = ggs, hip, ggs.parallel
     return ggs

@@ -28,13 +28,14 @@ from conftest import ORACLE, PKG, REPO
 sys.path.insert(0, REPO)
 
 
-def _rank_main(rank, world, mesh, argv, out_dir, slow_rank, corrupt):
+def _rank_main(rank, world, mesh, argv, out_dir, slow_rank, corrupt, stall=None):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT="29555",
                       GGS_RDZV_DIR=out_dir, GGS_RDZV_KEY="bench-dist-test")
+    sys.stderr = open(os.path.join(out_dir, f"stderr{rank}.txt"), "w", buffering=1)
     import _fakes
     log = {}
-    _fakes.install_fake_gpu(mesh, rank, world, log, slow_rank=slow_rank, corrupt=corrupt)
+    _fakes.install_fake_gpu(mesh, rank, world, log, slow_rank=slow_rank, corrupt=corrupt, stall=stall)
     import bench
     rc = 0
     with open(os.path.join(out_dir, f"stdout{rank}.txt"), "w") as f, contextlib.redirect_stdout(f):
@@ -49,11 +50,11 @@ def _rank_main(rank, world, mesh, argv, out_dir, slow_rank, corrupt):
     os._exit(rc)
 
 
-def _run_world(tmp_path, argv, world=2, slow_rank=1, corrupt=False):
+def _run_world(tmp_path, argv, world=2, slow_rank=1, corrupt=False, stall=None):
     import _fakes
     ctx = mp.get_context("fork")
     mesh = _fakes.PipeMesh(world, ctx)
-    procs = [ctx.Process(target=_rank_main, args=(r, world, mesh, argv, str(tmp_path), slow_rank, corrupt))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, mesh, argv, str(tmp_path), slow_rank, corrupt, stall))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -62,6 +63,8 @@ def _run_world(tmp_path, argv, world=2, slow_rank=1, corrupt=False):
         if p.is_alive():
             p.kill()
             raise TimeoutError("a rank hung")
+    if stall is not None:
+        return [p.exitcode for p in procs], None, None
     logs = [json.load(open(tmp_path / f"log{r}.json")) for r in range(world)]
     out0 = (tmp_path / "stdout0.txt").read_text().strip().splitlines()
     return [p.exitcode for p in procs], logs, out0
@@ -87,7 +90,7 @@ def test_bench_world2_orchestration(tmp_path):
     assert line["config"]["rccl_ranks"] == 2 and line["config"]["global_batch"] == 256
     assert line["config"]["fitness_gather"] == "rccl" and line["config"]["pop_per_gpu"] == 128
     assert line["timing"]["passes"] >= 1 and line["value"] > 0
-    assert line["roofline"]["binding"] == "valu" and line["roofline"]["bound"] == "hbm"
+    assert line["roofline"]["binding"] == "valu" and line["roofline"]["bound"] == "valu"
     pe = line["plan_excluded"]
     assert pe["device_api_unplanned_value"] > 0 and pe["plan_build_ms"] >= 0
     assert not (tmp_path / "stdout1.txt").read_text().strip()               # rank 1 prints nothing
@@ -103,6 +106,61 @@ def test_bench_world2_strong_scaling_splits_configs3(tmp_path):
     line = json.loads(out0[0])
     assert line["scaling"] == "strong" and line["n_gpus"] == 2
     assert line["config"]["global_batch"] == 4096 and line["config"]["pop_per_gpu"] == 2048
+
+
+@pytest.mark.parametrize("stall_at", [0, 9])
+def test_bench_world2_stalled_gather_fails_loudly_naming_the_rank(tmp_path, stall_at):
+    """Rank 1 never issues one fitness gather (its stand-in communicator blocks
+    forever in that call: gather 0 sits in the warm-up, gather 9 in the first timed
+    pass).  Rank 0 issues past it and waits in the pass's barrier.  Each rank's
+    watchdog fires at its phase deadline (floor 2 s here), every rank exits with
+    WATCHDOG_EXIT well before the stand-in transport's own 60 s timeout, and both
+    name rank 1 from the heartbeat files, with phase, step, stream and the
+    collectives issued on stderr."""
+    import time
+    import bench
+    t0 = time.monotonic()
+    codes, _, _ = _run_world(tmp_path, ["--gpus", "2", "--watchdog-floor-s", "2"] + FAST,
+                             stall=(1, stall_at))
+    took = time.monotonic() - t0
+    assert codes == [bench.WATCHDOG_EXIT] * 2
+    assert took < 30, took
+    for r in range(2):
+        err = (tmp_path / f"stderr{r}.txt").read_text()
+        assert f"bench.py watchdog: rank {r}: phase" in err, err
+        assert "stalled rank(s): [1]" in err, err
+        assert "rank 0: phase" in err and "rank 1: phase" in err and "issued" in err, err
+    assert "gather" not in (tmp_path / "stdout0.txt").read_text()            # no JSON line
+
+
+def test_watchdog_names_frozen_or_lagging_ranks():
+    import bench
+    now = 1000.0
+    hb = {r: {"wall": now, "issued_total": 12} for r in range(4)}
+    assert bench.Watchdog.stalled(hb, now, 5.0)[0] == []                       # a device hang
+    hb[2]["issued_total"] = 9
+    assert bench.Watchdog.stalled(hb, now, 5.0)[0] == [2]
+    hb[3] = None
+    assert bench.Watchdog.stalled(hb, now, 5.0)[0] == [3]
+    hb[3] = {"wall": now - 60, "issued_total": 12}
+    assert bench.Watchdog.stalled(hb, now, 5.0)[0] == [3]
+
+
+def test_stream_accounting_refuses_shared_queues():
+    import bench
+    a = bench.stream_accounting(4, True, "rccl", 8)
+    assert a["collective_streams"] == 5 and a["communicator_streams"] == 1 and a["ok"]
+    assert bench.stream_accounting(4, True, "rccl-overlap", 8)["collective_streams"] == 4
+    assert not bench.stream_accounting(8, True, "rccl", 8)["ok"]
+    w1 = bench.stream_accounting(4, False, "rccl", 4)
+    assert w1["collective_streams"] == 0 and w1["communicators"] == 0 and w1["ok"]
+
+
+def test_bench_refuses_more_collective_streams_than_queues(tmp_path, monkeypatch):
+    import bench
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    with pytest.raises(SystemExit, match="GPU_MAX_HW_QUEUES=8"):
+        bench.run(bench.parse_args(["--streams", "8"]), 2, 0, 0, True)
 
 
 def test_bench_world2_bad_gather_fails_the_shard_check(tmp_path):

@@ -133,3 +133,52 @@ def test_profile_config_matches_the_launch_shape():
     assert bench.profile_config("1024x8", 0, 512) == "1024"          # N = 8: configs[2]'s launch
     assert bench.profile_config("1024x8", 0, 2048) is None           # N = 2: not profiled
     assert bench.profile_config("512", 64, 64) is None               # --pop exploration
+
+
+def test_bench_line_names_its_roofs_and_value_semantics(tmp_path):
+    """The world-1 JSON line (bench.run on the stand-in GPU of tests/_fakes.py):
+    `bound` names the binding roof (VALU), achieved/peak/frac are the HBM figures
+    the contract defines (frac_roof), valu.frac is the executed-work PMC busy of
+    the committed profile (never the reference-equivalent FLOP ratio, which sits
+    under its own name), and the line says that `value` overlaps independent
+    batches while value_one_stream is a generation-by-generation caller's rate."""
+    import json
+    from test_bench_dist import FAST, _run_world
+    codes, _, out0 = _run_world(tmp_path, ["--gpus", "1"] + FAST, world=1, slow_rank=None)
+    assert codes == [0]
+    line = json.loads(out0[0])
+    roof, valu = line["roofline"], line["valu"]
+    assert roof["bound"] == "valu" and roof["binding"] == "valu" and roof["frac_roof"] == "hbm"
+    assert roof["unit"] == "GB/s" and roof["peak"] == bench.HBM_PEAK_GBS
+    assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-4
+    busy = bench.pmc_valu_busy()
+    assert valu["frac"] == busy == roof["binding_frac"] and 0 < busy < 1
+    assert valu["frac_source"].startswith("profiles/r") and "SQ_ACTIVE_INST_VALU" in valu["frac_definition"]
+    assert "frac" not in valu["reference_equivalent"] and "ratio_to_peak" in valu["reference_equivalent"]
+    sem = line["value_semantics"]
+    assert "independent populations" in sem and "value_one_stream" in sem and "algorithm.py:123-141" in sem
+    assert line["value_one_stream"] > 0 and line["value_with_readback"] > 0
+    assert line["config"]["rccl_ranks"] is None and line["n_gpus"] == 1
+
+
+def test_committed_profile_summaries_agree_with_themselves():
+    """Committed profiles/*/summary.json files do not contradict themselves:
+    only a bench.py profile (profiles/rNN, rNN_<config>) quotes a single-stream
+    profile-pass raster average (raster_profile_pass_avg_us, what the bench line
+    pairs with its live HIP-event figure), and that pass is never slower than the
+    trace's all-dispatch average beside it (which also holds the overlapped
+    multi-stream launches); a GA / SA loop profile has no such pass, so its
+    figure is the kernel table's."""
+    import glob
+    import json
+    for p in glob.glob(os.path.join(REPO, "profiles", "*", "summary.json")):
+        name = os.path.basename(os.path.dirname(p))
+        d = json.load(open(p))
+        pass_avg = d.get("raster_profile_pass_avg_us")
+        if "_sa" in name or "_ga" in name:
+            assert pass_avg is None, p
+            continue
+        if pass_avg is None:
+            continue
+        ks = [v["avg_us"] for k, v in d.get("kernels", {}).items() if "raster_kernel" in k]
+        assert len(ks) == 1 and pass_avg <= 1.02 * ks[0], (p, pass_avg, ks)

@@ -275,6 +275,34 @@ def test_fitness_vs_oracle_1024_config():
                                                              weight_mask=mask))
 
 
+def test_headline_config_matches_reference_golden():
+    """BASELINE.json configs[1] (512x512, 256 splats) pinned directly to the
+    reference (tests/golden/headline_512.npz, made by make_golden_512.py running
+    render.py's Triton kernel under the interpreter and fitness.py): libggs's full
+    image within 1e-4 abs of the reference's tile-64 image (render.py:203-252),
+    its weighted / plain / boost fitness within 1e-5 relative of fitness_many
+    (fitness.py:7-31), through the host API and the planned device path the bench
+    times (ggs_plan_create + fitness)."""
+    d = load_golden("headline_512.npz")
+    H, W = int(d["HWk"][0]), int(d["HWk"][1])
+    img = ggs.render(d["genomes"], H, W, k_sigma=float(d["HWk"][2]))
+    np.testing.assert_allclose(img, d["img_t64"], atol=IMG_TOL, rtol=0)
+    tgt = d["target_u8"].astype(np.float32) / np.float32(255.0)
+    for mode, kw in (("none", {}), ("weighted", {"weight_mask": d["mask"]}),
+                     ("boost", {"weight_mask": d["mask"], "boost_only": True})):
+        got = ggs.fitness(d["pop"], tgt, H, W, 3.0, **kw)
+        np.testing.assert_allclose(got, d[f"fit_{mode}"], rtol=FIT_RTOL, err_msg=mode)
+    from ggs import hip
+    st = hip.Stream()
+    g, t, m = (hip.DeviceArray.from_host(np.ascontiguousarray(a, np.float32)) for a in (d["pop"], tgt, d["mask"]))
+    out = hip.DeviceArray((1,))
+    plan = ggs.TargetPlan(0, st.handle, t.ptr, m.ptr, ggs.GGS_FIT_WEIGHTED, 1.0, H, W)
+    plan.fitness_device(st.handle, g.ptr, 1, d["pop"].shape[1], 9, 3.0, out.ptr)
+    st.synchronize()
+    np.testing.assert_allclose(out.to_host(), d["fit_weighted"], rtol=FIT_RTOL)
+    plan.close()
+
+
 @pytest.mark.parametrize("N", [512, 513])
 def test_ga_default_config_vs_oracle(N):
     """The reference's shipped GA run (run_ggs.py:41, config.py:5-11): 512^2 work

@@ -149,3 +149,28 @@ def test_oracle_window_render_equals_crop_of_full_render():
     for win in ((10, 57, 3, 66), (0, 100, 0, 70), (99, 100, 69, 70)):
         y0, y1, x0, x1 = win
         np.testing.assert_array_equal(O.render(G, 100, 70, window=win), full[:, y0:y1, x0:x1])
+
+
+def test_headline_config_matches_reference():
+    """BASELINE.json configs[1] itself (512x512, 256 splats): the oracle's encode,
+    full-canvas render and weighted / plain / boost fitness against the reference
+    run on the same candidate (tests/golden/make_golden_512.py: tile-64 image,
+    tile-32 fitness_many) — the headline config pinned directly, not only through
+    the small fixtures above."""
+    d = load_golden("headline_512.npz")
+    H, W, k = (float(v) for v in d["HWk"])
+    H, W = int(H), int(W)
+    g9, ref9 = O.genome_to_renderer_batched(d["pop"]), d["genomes"]
+    np.testing.assert_array_equal(g9[..., :2], ref9[..., :2])
+    np.testing.assert_array_equal(g9[..., 5:], ref9[..., 5:])
+    kappa = _l22_condition(d["pop"]).reshape(ref9.shape[:-1])       # as test_encode_matches_reference
+    for col in (2, 3, 4):
+        tol = 16 * EPS * (1 + np.abs(ref9[..., col])) * np.maximum(kappa, 1.0)
+        assert (np.abs(g9[..., col].astype(np.float64) - ref9[..., col]) <= tol).all(), col
+    img = O.render(d["genomes"], H, W, k_sigma=k)
+    np.testing.assert_allclose(img, d["img_t64"], atol=1e-5, rtol=0)
+    tgt = d["target_u8"].astype(np.float32) / np.float32(255.0)
+    for mode, kw in (("none", {}), ("weighted", {"weight_mask": d["mask"]}),
+                     ("boost", {"weight_mask": d["mask"], "boost_only": True})):
+        got = O.fitness_many(list(d["pop"]), tgt, H, W, k, **kw)
+        np.testing.assert_allclose(got, d[f"fit_{mode}"], rtol=1e-5, err_msg=mode)
