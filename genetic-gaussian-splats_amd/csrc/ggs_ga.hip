@@ -282,11 +282,12 @@ __device__ unsigned long long g_ggs_vtiming[8 * 4096];
 #define GGS_VMARK(k) do { } while (0)
 #endif
 
-// Threads per variation workgroup (one workgroup per offspring): 256 for a GA
-// generation (P workgroups fill the chip); 1024 when a few large offspring are
-// bred (SA tries at configs[4]: 4,096 splats each), which otherwise leave 16
-// splats per thread on a handful of CUs.  Results do not depend on VT (per-splat
-// work, an OR, a sum and an in-order search).
+// Threads per variation workgroup (one workgroup per offspring): the smallest of
+// 256 / 512 / 1024 that gives every splat its own thread up to 1,024 splats (the
+// register-resident path below); 256 past that, and 1024 when a few large
+// offspring are bred (SA tries at configs[4]: 4,096 splats each), which otherwise
+// leave 16 splats per thread on a handful of CUs.  Results do not depend on VT
+// (per-splat work, an OR, a sum and an in-order search).
 //
 // BREED: the generation's survivors and gather run inside this kernel (one extra
 // workgroup, o == n_off, keeps best and curves): the parents are the rows of the
@@ -842,17 +843,27 @@ hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fi
                                float* off, int n_off, SplatRec* recs, int4* bnds, int H, int W, float k_sigma,
                                const SaLoopDev* sl, const SaItDev* sit, const BreedDev* br) {
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    // The smallest workgroup that holds one splat per thread (the register-resident
+    // path, N <= VT) up to 1,024 splats: the shipped GA run (config.py: 512 splats)
+    // on the generic path (two splats per thread, the child rows round-tripping
+    // through HBM between the passes) bred in 21.6 us per generation.
+    const int vt = N <= 256 ? 256 : N <= 512 ? 512 : 1024;
+#define GGS_VAR(VTT, BR, NB, BD)                                                                  \
+    hipLaunchKernelGGL((ga_variation_kernel<VTT, BR>), dim3(NB), dim3(VTT), 0, st, pop, fits, P, N, prm, d, k0, \
+                       k1, gen, off, n_off, recs, bnds, H, W, k_sigma, sl, sit, BD)
     if (br) {       // + the stats workgroup
         if (P > RANKMAX || n_off != P) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((ga_variation_kernel<256, true>), dim3(n_off + 1), dim3(256), 0, st, pop, fits, P, N,
-                           prm, d, k0, k1, gen, off, n_off, recs, bnds, H, W, k_sigma, sl, sit, *br);
-    } else if (n_off < 64 && N >= 1024) {
-        hipLaunchKernelGGL((ga_variation_kernel<1024, false>), dim3(n_off), dim3(1024), 0, st, pop, fits, P, N,
-                           prm, d, k0, k1, gen, off, n_off, recs, bnds, H, W, k_sigma, sl, sit, BreedDev{});
+        if (vt == 256) GGS_VAR(256, true, n_off + 1, *br);
+        else if (vt == 512) GGS_VAR(512, true, n_off + 1, *br);
+        else GGS_VAR(1024, true, n_off + 1, *br);
+    } else if ((n_off < 64 && N >= 1024) || (N > 512 && N <= 1024)) {
+        GGS_VAR(1024, false, n_off, BreedDev{});
+    } else if (N > 256 && N <= 512) {
+        GGS_VAR(512, false, n_off, BreedDev{});
     } else {
-        hipLaunchKernelGGL((ga_variation_kernel<256, false>), dim3(n_off), dim3(256), 0, st, pop, fits, P, N,
-                           prm, d, k0, k1, gen, off, n_off, recs, bnds, H, W, k_sigma, sl, sit, BreedDev{});
+        GGS_VAR(256, false, n_off, BreedDev{});
     }
+#undef GGS_VAR
     return hipGetLastError();
 }
 

@@ -39,7 +39,10 @@ def _problem(H, W, seed):
 
 @pytest.mark.parametrize("H,W,P,N,G,tour_k,elite_k,cxpb,mutpb,boost,seed", [
     (40, 40, 17, 33, 4, 3, 4, 0.5, 0.2, False, 1),     # odd P (last pair yields one child)
-    (64, 48, 32, 300, 3, 2, 8, 0.9, 0.05, True, 2),    # N > 256: multi-pass workgroup loops
+    (64, 48, 32, 300, 3, 2, 8, 0.9, 0.05, True, 2),    # 256 < N <= 512: 512-thread breed workgroups
+    (64, 64, 32, 512, 3, 2, 8, 0.05, 0.05, False, 6),  # config.py's shape: N 512, pop 32, elite 8
+    (40, 40, 12, 700, 2, 2, 2, 0.5, 0.1, False, 7),    # 512 < N <= 1024: 1024-thread workgroups
+    (32, 40, 10, 1100, 2, 2, 2, 0.5, 0.1, True, 8),    # N > 1024: generic multi-pass workgroup loops
     (32, 32, 8, 2, 5, 2, 1, 0.3, 0.01, False, 3),      # N = 2, rare mutation -> fallbacks
     (24, 24, 6, 1, 3, 2, 0, 0.5, 0.5, False, 4),       # N = 1: no swap; elite_k 0 -> 1
     (16, 16, 600, 3, 2, 3, 25, 0.5, 0.1, False, 5),    # P > 512: bitonic survivors path
@@ -143,10 +146,11 @@ from ggs import ga
 from ggs.ga_device import DeviceGA
 from ggs.mask import compute_importance_mask, prepare_target
 H = W = 512
+P, N = int(sys.argv[3]), int(sys.argv[4])
 target = np.random.default_rng(0).uniform(0, 255, (H, W, 3)).astype(np.float32)
 t = prepare_target(target, H, W)
 m = compute_importance_mask(t, H, W, smooth=3, strength=0.7)
-init = ga.new_population(128, 256, H, W, 3.0, 0.1, np.random.default_rng(0))
+init = ga.new_population(P, N, H, W, 3.0, 0.1, np.random.default_rng(0))
 cfg = dict(mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0, "alpha": 25.0},
            mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0, "alpha": 2.0},
            schedule="cosine")
@@ -159,10 +163,12 @@ np.savez(sys.argv[2], population=st["population"], fitness=st["fitness"], best=s
 """
 
 
-def test_device_ga_fused_breed_equals_unfused(tmp_path):
+@pytest.mark.parametrize("P,N", [(128, 256), (32, 512)])
+def test_device_ga_fused_breed_equals_unfused(tmp_path, P, N):
     """The fused breed (survivors + gather inside the variation kernel) against the
-    five-launch generation (GGS_GA_UNFUSED=1) at the bench workload, 25 generations
-    of Philox draws in one run: identical populations, fitness, best and curves."""
+    five-launch generation (GGS_GA_UNFUSED=1) at the bench workload and at the
+    reference's shipped run (config.py: 512 splats, pop 32), 25 generations of
+    Philox draws in one run: identical populations, fitness, best and curves."""
     import os
     import subprocess
     import sys
@@ -170,7 +176,7 @@ def test_device_ga_fused_breed_equals_unfused(tmp_path):
     out = {}
     for tag, env in (("fused", {}), ("unfused", {"GGS_GA_UNFUSED": "1"})):
         path = str(tmp_path / f"{tag}.npz")
-        subprocess.run([sys.executable, "-c", _FUSED_SCRIPT, pkg, path], check=True, timeout=300,
+        subprocess.run([sys.executable, "-c", _FUSED_SCRIPT, pkg, path, str(P), str(N)], check=True, timeout=300,
                        env=dict(os.environ, **env))
         out[tag] = np.load(path)
     for k in out["fused"].files:
