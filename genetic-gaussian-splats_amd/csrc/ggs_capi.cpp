@@ -78,6 +78,25 @@ int ensure(DevBuf& b, size_t bytes, hipStream_t st) {
     return GGS_OK;
 }
 
+// ensure() for a counter block: a grown buffer is zeroed on `st` (the fused
+// finalize's per-candidate counters start at zero and every launch leaves them
+// at zero).
+int ensure_zeroed(DevBuf& b, size_t bytes, hipStream_t st) {
+    if (bytes <= b.cap) return GGS_OK;
+    int rc = ensure(b, bytes, st);
+    if (rc) return rc;
+    GGS_HIP(hipMemsetAsync(b.p, 0, b.cap, st));
+    return GGS_OK;
+}
+
+// The fitness finalize runs inside the raster (FinFused: the last strip wave of
+// each candidate reduces it), saving a launch per evaluation; GGS_UNFUSED_FINALIZE=1
+// restores the separate finalize_kernel launch (A/B switch, same bits).
+bool finalize_fused() {
+    static const bool off = getenv("GGS_UNFUSED_FINALIZE") && atoi(getenv("GGS_UNFUSED_FINALIZE")) != 0;
+    return !off;
+}
+
 struct PinBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -99,7 +118,7 @@ int ensure_pinned(PinBuf& b, size_t bytes) {
 // Per-(device, stream) scratch used by one render/fitness pipeline.
 struct Workspace {
     hipStream_t stream = nullptr;
-    DevBuf recs, bnds, partials, wpartials, order, plan;
+    DevBuf recs, bnds, partials, wpartials, order, plan, fctr;   // fctr: fused-finalize counters
     int order_H = -1, order_W = -1;   // (H, W) the tile order was built for
     uint64_t plan_key = 0;            // inputs the plan was built from (0: none / volatile)
 };
@@ -182,6 +201,40 @@ void prof_drain_locked() {
         (void)hipEventDestroy(r.b);
     }
     g_prof_pending.clear();
+}
+
+// raster (MODE 1) + finalize of B candidates: one launch when fused.
+int raster_fitness(hipStream_t st, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
+                   const float4* plan, float* partials, const float* wpartials, int mode, const int* order,
+                   DevBuf& ctr, float* out, const unsigned char* dirty = nullptr, const float* clean = nullptr) {
+    const float bg[3] = {1.f, 1.f, 1.f};  // fitness renders with the default background (fitness.py:15)
+    int nTX;
+    const int nTiles = raster_tiles(H, W, &nTX);
+    // fused only where every candidate's partials fill whole 128-B lines (4 * nTiles
+    // a multiple of 32 floats: 512^2, 1024^2, 2048^2 ...): a line is then read, with
+    // agent-scope loads, by one wave only, after every store to it, and never sits
+    // in that XCD's L2 from an earlier read of a neighbour candidate's finalize
+    if (finalize_fused() && (4 * nTiles) % 32 == 0) {
+        int rc;
+        if ((rc = ensure_zeroed(ctr, sizeof(int) * (size_t)std::max(B, 1), st))) return rc;
+        FinFused ff;
+        ff.ctr = (int*)ctr.p;
+        ff.wpartials = wpartials;
+        ff.out = out;
+        ff.hw = (double)H * (double)W;
+        ff.mode = mode;
+        ProfScope ps(st, 1);
+        GGS_HIP(launch_raster(st, 1, recs, bnds, B, N, H, W, bg, nullptr, plan, partials, order, dirty, clean,
+                              nullptr, &ff));
+        return GGS_OK;
+    }
+    {
+        ProfScope ps(st, 1);
+        GGS_HIP(launch_raster(st, 1, recs, bnds, B, N, H, W, bg, nullptr, plan, partials, order, dirty, clean));
+    }
+    ProfScope ps(st, 2);
+    GGS_HIP(launch_finalize(st, partials, wpartials, B, nTiles, mode, H, W, out));
+    return GGS_OK;
 }
 
 // ---- helpers ----------------------------------------------------------------------
@@ -352,19 +405,8 @@ int run_fitness_planned(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B
         ProfScope ps(st, 0);
         GGS_HIP(launch_prep(st, true, d_gen, B * N, C, H, W, k, recs, (int4*)w->bnds.p, nullptr, nullptr, nullptr));
     }
-    const float bg[3] = {1.f, 1.f, 1.f};  // fitness renders with the default background (fitness.py:15)
-    {
-        ProfScope ps(st, 1);
-        GGS_HIP(launch_raster(st, 1, recs, (const int4*)w->bnds.p, (int)B, N, H, W, bg, nullptr, plan,
-                              (float*)w->partials.p,
-                              (const int*)w->order.p));
-    }
-    {
-        ProfScope ps(st, 2);
-        GGS_HIP(launch_finalize(st, (const float*)w->partials.p, wpartials, (int)B, nTiles, mode, H, W,
-                                d_out));
-    }
-    return GGS_OK;
+    return raster_fitness(st, recs, (const int4*)w->bnds.p, (int)B, N, H, W, plan, (float*)w->partials.p,
+                          wpartials, mode, (const int*)w->order.p, w->fctr, d_out);
 }
 
 int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, int C, int H, int W,
@@ -479,7 +521,7 @@ void ggs_shutdown(void) {
         (void)hipStreamSynchronize(c->stream);
         for (auto& w : c->ws) {
             if (w->stream) (void)hipStreamSynchronize(w->stream);
-            for (DevBuf* b : {&w->recs, &w->bnds, &w->partials, &w->wpartials, &w->order, &w->plan})
+            for (DevBuf* b : {&w->recs, &w->bnds, &w->partials, &w->wpartials, &w->order, &w->plan, &w->fctr})
                 if (b->p) (void)hipFree(b->p);
         }
         for (DevBuf* b : {&c->gen, &c->out, &c->target, &c->mask})
@@ -943,7 +985,7 @@ struct GaSession {
     DevBuf elite[2];               // elite[cur]: rows of pop[cur] by fitness rank (the breed's row map)
     int ocur = 0;                  // off[ocur]: the offspring evaluated last
     bool pending = false;          // their survivors / gather not applied yet (ga_flush)
-    DevBuf recs, bnds, partials, plan, wpart, order;   // the generation's fused pipeline
+    DevBuf recs, bnds, partials, plan, wpart, order, fctr;   // the generation's fused pipeline
     int64_t n_curves = 0, curves_cap = 0;
     void* comm = nullptr;          // ggs_ga_set_comm: offspring fitness sharded over ranks
     int nranks = 1, rank = 0;
@@ -1094,7 +1136,6 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     }
     s->ocur = onew;
     s->pending = true;
-    const float bg[3] = {1.f, 1.f, 1.f};
     // Only offspring[:P - E] survive (algorithm.py:140-141: the next generation is the
     // E elites + the first P - E offspring, fitnesses likewise); the last E offspring's
     // fitness is never read (survivors, fused breed, best, curves), so they are bred
@@ -1104,20 +1145,12 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     // every rank bred all P offspring above with the same draws
     const int per = (Pe + s->nranks - 1) / s->nranks;
     const int b0 = std::min(Pe, s->rank * per), nb = std::min(Pe, b0 + per) - b0;
-    if (nb > 0) {
-        {
-            ProfScope ps(s->st, 1);
-            GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->recs.p + (int64_t)b0 * N,
-                                  (const int4*)s->bnds.p + (int64_t)b0 * N, nb, N, c.H, c.W, bg,
-                                  nullptr, (const float4*)s->plan.p, (float*)s->partials.p,
-                                  (const int*)s->order.p));
-        }
-        {
-            ProfScope ps(s->st, 2);
-            GGS_HIP(launch_finalize(s->st, (const float*)s->partials.p, (const float*)s->wpart.p, nb,
-                                    s->nTiles, c.fitness_mode, c.H, c.W, (float*)s->off_fits.p + b0));
-        }
-    }
+    if (nb > 0 && (rc = raster_fitness(s->st, (const SplatRec*)s->recs.p + (int64_t)b0 * N,
+                                       (const int4*)s->bnds.p + (int64_t)b0 * N, nb, N, c.H, c.W,
+                                       (const float4*)s->plan.p, (float*)s->partials.p, (const float*)s->wpart.p,
+                                       c.fitness_mode, (const int*)s->order.p, s->fctr,
+                                       (float*)s->off_fits.p + b0)))
+        return rc;
     if (s->comm && per > 0) {   // one in-place all-gather of the shards' fitness scalars (RCCL, same stream)
         float* of = (float*)s->off_fits.p;
         if ((rc = ggs_comm_allgather(s->comm, s->st, of + (int64_t)s->rank * per, of, per, 0, nullptr)))
@@ -1139,7 +1172,7 @@ struct SaSession {
     int N = 0, cap = 0, last_n = 0, nTiles = 0;
     bool incremental = false;   // measured slower at every SA config tried
     DevBuf curr, best, nb, nb_fits, target, mask, draws;
-    DevBuf cur_recs, nb_recs, nb_bnds, cur_part, nb_part, dirty, plan, wpart, order, counters;
+    DevBuf cur_recs, nb_recs, nb_bnds, cur_part, nb_part, dirty, plan, wpart, order, counters, fctr;
     DevBuf loop, sit, curves;       // device SA loop (ggs_sa_run): state, per-iteration table, curves
     DevBuf flags, sizes;            // ... and its mutation scratch (per-try mask-group flags, splat sizes)
     float* h_fits = nullptr;        // pinned
@@ -1152,7 +1185,8 @@ struct SaSession {
 void sa_free(SaSession* s) {
     for (DevBuf* b : {&s->curr, &s->best, &s->nb, &s->nb_fits, &s->target, &s->mask, &s->draws,
                       &s->cur_recs, &s->nb_recs, &s->nb_bnds, &s->cur_part, &s->nb_part, &s->dirty, &s->plan,
-                      &s->wpart, &s->order, &s->counters, &s->loop, &s->sit, &s->curves, &s->flags, &s->sizes})
+                      &s->wpart, &s->order, &s->counters, &s->loop, &s->sit, &s->curves, &s->flags, &s->sizes,
+                      &s->fctr})
         if (b->p) (void)hipFree(b->p);
     if (s->h_loop) (void)hipHostFree(s->h_loop);
     if (s->h_fits) (void)hipHostFree(s->h_fits);
@@ -1174,19 +1208,9 @@ int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, int4* bnds, flo
     if (dirty)
         GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, G, (const SplatRec*)s->cur_recs.p, recs, n,
                              s->N, c.H, c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p));
-    const float bg[3] = {1.f, 1.f, 1.f};
-    {
-        ProfScope ps(s->st, 1);
-        GGS_HIP(launch_raster(s->st, 1, recs, bnds, n, s->N, c.H, c.W, bg, nullptr, (const float4*)s->plan.p, part,
-                              (const int*)s->order.p, dirty ? (const unsigned char*)s->dirty.p : nullptr,
-                              (const float*)s->cur_part.p));
-    }
-    {
-        ProfScope ps(s->st, 2);
-        GGS_HIP(launch_finalize(s->st, part, (const float*)s->wpart.p, n, s->nTiles, c.fitness_mode, c.H, c.W,
-                                fits));
-    }
-    return GGS_OK;
+    return raster_fitness(s->st, recs, bnds, n, s->N, c.H, c.W, (const float4*)s->plan.p, part,
+                          (const float*)s->wpart.p, c.fitness_mode, (const int*)s->order.p, s->fctr, fits,
+                          dirty ? (const unsigned char*)s->dirty.p : nullptr, (const float*)s->cur_part.p);
 }
 
 // Shared validation of ggs_ga_create / ggs_sa_create.
@@ -1214,7 +1238,8 @@ void ga_free(GaSession* s) {
     for (DevBuf* b : {&s->pop[0], &s->pop[1], &s->fits[0], &s->fits[1], &s->off[0], &s->off[1], &s->off_fits,
                       &s->src, &s->elite[0], &s->elite[1],
                       &s->target, &s->mask, &s->best_ind, &s->best_fit, &s->best_src, &s->best_upd,
-                      &s->curves, &s->draws, &s->recs, &s->bnds, &s->partials, &s->plan, &s->wpart, &s->order})
+                      &s->curves, &s->draws, &s->recs, &s->bnds, &s->partials, &s->plan, &s->wpart, &s->order,
+                      &s->fctr})
         if (b->p) (void)hipFree(b->p);
     if (s->st) (void)hipStreamDestroy(s->st);
 }

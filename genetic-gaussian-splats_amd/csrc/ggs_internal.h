@@ -48,10 +48,24 @@ hipError_t launch_prep(hipStream_t st, bool encode, const float* genomes, int64_
                        int W, float k, SplatRec* recs, int4* bnds, float* f9, int* i4, float* enc9,
                        const int* live = nullptr, int n_per = 0);
 int raster_tiles(int H, int W, int* nTX);
+// The fitness finalize folded into the raster (MODE 1): each strip wave counts
+// itself in ctr[b] after storing its partial, and the candidate's last strip
+// wave reduces the candidate's partials (finalize_wave, so the same bits as
+// finalize_kernel) into out[b] and resets ctr[b] to 0 for the next launch.
+// ctr: one int per candidate of the launch, all zero before the first launch
+// (ensure_zeroed); the counters are per workspace, so launches that may run at
+// the same time (other streams) never share them.
+struct FinFused {
+    int* ctr = nullptr;               // null: no fusion (launch_finalize follows)
+    const float* wpartials = nullptr;  // the plan's weight block
+    float* out = nullptr;             // [B] fitness scalars
+    double hw = 0.0;                  // H * W
+    int mode = 0;                     // GGS_FIT_*
+};
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty = nullptr,
-                         const float* clean = nullptr, const int* live = nullptr);
+                         const float* clean = nullptr, const int* live = nullptr, const FinFused* fin = nullptr);
 // Strips touched by splats that differ between `nb` [n][N][9] and `curr` [N][9]
 // (old AABB from cur_recs, new from nb_recs) -> dirty [n][tiles][4] (zeroed first).
 hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, const SplatRec* cur_recs,

@@ -23,8 +23,11 @@
 //            clamp, then either the image store (render) or the weighted squared
 //            error against the target plan, summed per strip (the image never
 //            touches HBM).
-//   finalize 1 workgroup / candidate: fixed-order float64 sum of the strip
-//            partials -> the fitness scalar (deterministic, no atomics).
+//   finalize fixed-order float64 sum of a candidate's strip partials -> the
+//            fitness scalar (deterministic: the order never depends on which
+//            wave finished last).  Folded into the raster where the caller
+//            hands it a counter block (FinFused: the candidate's last strip
+//            wave reduces), else its own launch, one wave per candidate.
 //   plan     1 wave / (tile, strip): target + mode weights in raster lane order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -101,11 +104,11 @@ constexpr int OCC = 3;            // waves per SIMD the register budget is sized
 // each strip's plan slice once: 54 vs 80 MB of fabric traffic per launch, raster
 // -0.5 %; at 1024^2/1024 (33 MB of records) the 8-group rotation is 0.6 % faster)
 constexpr int XCD_SHIFT = 3;
-constexpr int CULL_PRIO = 2;
+constexpr int CULL_PRIO = 2;      // s_setprio while culling (1 and 3 measured the same)
 
 #ifndef GGS_NOPLAN
 #define GGS_NOPLAN 0      // diagnostic build (tools/probe/traffic_ab.sh): the epilogue reads no plan
-#endif      // s_setprio while culling (1 and 3 measured the same)
+#endif
 
 // Saturation cut-off.  Front to back, a strip's pixels receive Σ_rest T·f·c +
 // T_end·bg ≤ T from all the splats still to come (Σ w + T_end = T, c, bg ≤ 1).
@@ -141,6 +144,34 @@ constexpr int SAT_MIN_SPLATS = 512;          // launches with fewer splats use t
 constexpr int SAT_BATCH = GGS_SAT_BATCH;
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// One strip's partial (lane 0): an agent-scope store, written through to the
+// device coherence point, where a fused finalize on another XCD reads it.
+__device__ __forceinline__ void store_partial(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The fused finalize (FinFused), after lane 0 stored this strip's partial.  The
+// partial is the only data another wave reads, and its agent-scope store is
+// written through: waiting for that store (vmcnt(0)) before the count orders it,
+// so the add itself is relaxed.  (A release add also writes back the whole L2
+// (buffer_wbl2) in every wave: raster 0.159 -> 0.351 ms at 512^2/256/pop 128.)
+// The wave whose add completes the candidate's count reduces all its partials
+// with agent-scope loads (the same finalize_wave arithmetic as finalize_kernel,
+// so the same bits whichever wave is last) and re-arms the counter.
+__device__ __forceinline__ void strip_done(const FinFused& fin, const float* partials, int b, int nslots,
+                                           int lane) {
+    int old = 0;
+    if (lane == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        old = __hip_atomic_fetch_add(fin.ctr + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (ufirst(old) != nslots - 1) return;
+    const float v = finalize_wave<true>(partials, fin.wpartials, nslots, fin.mode, fin.hw, b);
+    if (lane == 0) {
+        fin.out[b] = v;
+        __hip_atomic_store(fin.ctr + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 #ifndef GGS_TIMING
 #define GGS_TIMING 0              // diagnostic build: per-wave phase clocks (tools/probe/wave_timing.py)
@@ -252,7 +283,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
-              const float* __restrict__ clean, const int* __restrict__ live, int CH) {
+              const float* __restrict__ clean, const int* __restrict__ live, int CH, FinFused fin) {
     __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
 
     const int lane = threadIdx.x & 63;
@@ -298,7 +329,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     if (MODE != 0 && dirty) {         // incremental (SA): a strip no changed splat touches
         const int64_t slot = ((int64_t)b * nTiles + t) * 4 + wv;   // keeps the current state's
         if (!dirty[slot]) {                                         // partial, bit for bit
-            if (lane == 0) partials[slot] = clean[t * 4 + wv];
+            if (lane == 0) store_partial(partials + slot, clean[t * 4 + wv]);
+            if (fin.ctr) strip_done(fin, partials, b, nTiles * 4, lane);
             return;
         }
     }
@@ -565,6 +597,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             }
         done:;
         };
+#undef rows_from
+#undef rows_upto
         // two records in alternating SGPR sets: the next record is loaded into
         // the set the finished visit used, so no register rotation at the latch
         auto load_at = [&](int jj) __attribute__((always_inline)) {
@@ -662,7 +696,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if (lane == 0)        // one partial per (candidate, tile, strip): no block barrier
-            partials[((int64_t)b * nTiles + t) * 4 + wv] = acc;
+            store_partial(partials + ((int64_t)b * nTiles + t) * 4 + wv, acc);
+        if (fin.ctr) strip_done(fin, partials, b, nTiles * 4, lane);
     }
 #if GGS_TIMING
     {
@@ -901,14 +936,15 @@ int raster_chunk(int N) {
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty, const float* clean,
-                         const int* live) {
+                         const int* live, const FinFused* fin) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
     const int CH = raster_chunk(N);
+    const FinFused ff = (mode != 0 && fin) ? *fin : FinFused{};
 #define GGS_RASTER(M, S)                                                                       \
     hipLaunchKernelGGL((raster_kernel<M, S>), grid, block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
-                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH)
+                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH, ff)
     // the saturation check only where strip lists can grow long (N > SAT_MIN_SPLATS);
     // at the bench's 256 splats the kernel without it is the faster code (+1.6 %)
     const bool sat = N > SAT_MIN_SPLATS;

@@ -127,6 +127,15 @@ __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
 // bits: a+b == b+a).  Strip partials give the numerator, the plan's per-strip
 // weight sums the denominator.  finalize_kernel and the GA's survivors kernel
 // both call this, so the fitness of a candidate has the same bits either way.
+// COHERENT: the partials were written by waves of the SAME launch, possibly on
+// other XCDs (the raster's fused finalize): agent-scope loads (sc1) read them at
+// the device coherence point, past this XCD's L2.  Same adds, same bits.
+template <bool COHERENT = false>
+__device__ __forceinline__ float ld_partial(const float* __restrict__ p) {
+    if (COHERENT) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *p;
+}
+template <bool COHERENT = false>
 __device__ __forceinline__ double wave_sum(const float* __restrict__ x, int n) {
     const int lane = threadIdx.x & 63;
     double a = 0.0;
@@ -137,27 +146,28 @@ __device__ __forceinline__ double wave_sum(const float* __restrict__ x, int n) {
     for (; i + 31 * 64 < n; i += 32 * 64) {
         float v[32];
 #pragma unroll
-        for (int k = 0; k < 32; ++k) v[k] = x[i + k * 64];
+        for (int k = 0; k < 32; ++k) v[k] = ld_partial<COHERENT>(x + i + k * 64);
 #pragma unroll
         for (int k = 0; k < 32; ++k) a += (double)v[k];
     }
     for (; i + 7 * 64 < n; i += 8 * 64) {
         float v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = x[i + k * 64];
+        for (int k = 0; k < 8; ++k) v[k] = ld_partial<COHERENT>(x + i + k * 64);
 #pragma unroll
         for (int k = 0; k < 8; ++k) a += (double)v[k];
     }
-    for (; i < n; i += 64) a += (double)x[i];
+    for (; i < n; i += 64) a += (double)ld_partial<COHERENT>(x + i);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
     return a;
 }
 
+template <bool COHERENT = false>
 __device__ __forceinline__ float finalize_wave(const float* __restrict__ partials,
                                                const float* __restrict__ wpartials, int nT, int mode,
                                                double hw, int b) {
-    const double num = wave_sum(partials + (int64_t)b * nT, nT);
+    const double num = wave_sum<COHERENT>(partials + (int64_t)b * nT, nT);
     // wpartials: the plan's weight block, Sum w (float64) first (plan_wsum_kernel)
     const double wsum = mode != GGS_FIT_NONE ? *reinterpret_cast<const double*>(wpartials) : 0.0;
     double v;

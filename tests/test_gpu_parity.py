@@ -303,6 +303,40 @@ def test_headline_config_matches_reference_golden():
     plan.close()
 
 
+def test_fused_finalize_bit_stable_under_concurrent_uneven_load():
+    """The finalize folded into the raster (the last strip wave of each candidate
+    reduces the partials other waves, on any XCD, stored write-through; agent-scope
+    loads, no fence) under uneven concurrent load: four streams with their own
+    plans and workspaces, batches of 128 / 37 / 1 candidates at 512^2 and 24 at
+    1024^2, 30 launches each, enqueued interleaved with no sync; every launch's
+    fitness vector equals, bit for bit, the same batch evaluated alone — and the
+    per-candidate counters re-arm (a second round of launches agrees too)."""
+    from ggs import hip
+    rng = np.random.default_rng(77)
+    jobs = []
+    for H, B, seed in ((512, 128, 1), (512, 37, 2), (512, 1, 3), (1024, 24, 4)):
+        pop = O.synthetic_population(B, 256 if H == 512 else 512, H, H, seed=seed)
+        tgt = rng.uniform(0, 1, (H, H, 3)).astype(np.float32)
+        mask = rng.uniform(0.4, 1.0, (H, H)).astype(np.float32)
+        st = hip.Stream()
+        g, t, m = (hip.DeviceArray.from_host(a) for a in (pop, tgt, mask))
+        plan = ggs.TargetPlan(0, st.handle, t.ptr, m.ptr, ggs.GGS_FIT_WEIGHTED, 1.0, H, H)
+        jobs.append(dict(H=H, B=B, N=pop.shape[1], st=st, g=g, t=t, m=m, plan=plan,
+                         alone=ggs.fitness(pop, tgt, H, H, 3.0, weight_mask=mask)))
+    for _ in range(2):
+        outs = [[hip.DeviceArray((j["B"],)) for _ in range(30)] for j in jobs]
+        for i in range(30):
+            for j, o in zip(jobs, outs):
+                j["plan"].fitness_device(j["st"].handle, j["g"].ptr, j["B"], j["N"], 9, 3.0, o[i].ptr)
+        for j in jobs:
+            j["st"].synchronize()
+        for j, o in zip(jobs, outs):
+            for i in range(30):
+                np.testing.assert_array_equal(o[i].to_host(), j["alone"], err_msg=f"H={j['H']} B={j['B']} #{i}")
+    for j in jobs:
+        j["plan"].close()
+
+
 @pytest.mark.parametrize("N", [512, 513])
 def test_ga_default_config_vs_oracle(N):
     """The reference's shipped GA run (run_ggs.py:41, config.py:5-11): 512^2 work
