@@ -1171,6 +1171,10 @@ struct SaSession {
     ggs_ga_config cfg{};
     int N = 0, cap = 0, last_n = 0, nTiles = 0;
     bool incremental = false;   // measured slower at every SA config tried
+    // cur_recs / cur_part describe the current state (create evaluates them, commit and
+    // an incremental device run install them); a non-incremental ggs_sa_run may
+    // accept neighbours without installing them
+    bool cur_cache_valid = true;
     DevBuf curr, best, nb, nb_fits, target, mask, draws;
     DevBuf cur_recs, nb_recs, nb_bnds, cur_part, nb_part, dirty, plan, wpart, order, counters, fctr;
     DevBuf loop, sit, curves;       // device SA loop (ggs_sa_run): state, per-iteration table, curves
@@ -1578,6 +1582,7 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
     std::lock_guard<std::mutex> lk(s->c->mu);
     DeviceGuard dg(s->c->dev);
     s->driver = 2;
+    if (!s->incremental) s->cur_cache_valid = false;
     const ggs_ga_config& c = s->cfg;
     std::vector<SaItDev> tab((size_t)n_its);
     for (int i = 0; i < n_its; ++i) {
@@ -1733,16 +1738,18 @@ int ggs_sa_set_incremental(void* handle, int32_t on) {
     if (!handle) return fail(GGS_EINVAL, "null handle");
     SaSession* s = (SaSession*)handle;
     std::lock_guard<std::mutex> lk(s->c->mu);
-    if (on && !s->incremental) {
+    if (on && !s->incremental && !s->cur_cache_valid) {
         // The device loop installs an accepted neighbour's records and strip
         // partials only while incremental evaluation is on (sa_accept_kernel), so
         // after an incremental-off ggs_sa_run they describe an older state:
         // re-evaluate the current state before the dirty-strip test relies on them.
+        // (Right after create, or after propose/commit, they are current: no work.)
         DeviceGuard dg(s->c->dev);
         int rc = sa_eval(s, (const float*)s->curr.p, 1, (SplatRec*)s->cur_recs.p, (int4*)s->nb_bnds.p,
                          (float*)s->cur_part.p, (float*)s->nb_fits.p, false);
         if (rc) return rc;
         GGS_HIP(hipStreamSynchronize(s->st));
+        s->cur_cache_valid = true;
     }
     s->incremental = on != 0;
     return GGS_OK;

@@ -70,7 +70,14 @@ def _on_devices(device, n_devices: int):
     library's device list in between).  n_devices == 1 (default): the single
     device ``device`` names; n_devices > 1: fan the batch out over the first
     n_devices GPUs (opt-in; one RCCL gather returns the scalars); n_devices <= 0:
-    all GPUs."""
+    all GPUs.
+
+    The lock is process-wide and held for the whole C call, so the host API
+    (render / fitness / encode / preprocess) is serialised across Python threads:
+    concurrent host-API calls run one after another (the library's per-device
+    pipeline is one stream anyway).  Threads that want concurrent GPU work use the
+    device-pointer API (``fitness_device`` / ``TargetPlan`` on their own HIP
+    streams), which takes no such lock."""
     n = _lib.ensure_init()
     if n_devices == 1:
         ids = (device_index(device),)

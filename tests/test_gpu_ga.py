@@ -383,3 +383,40 @@ def test_device_loop_incremental_equals_full_at_configs4_size():
     np.testing.assert_array_equal(s1["current"], s0["current"])
     assert f1 == f0 and s1["curves"] == s0["curves"]
     assert 0 < s1["stats"]["changed_splats"] < s1["stats"]["proposed"] * 4096 // 4
+
+
+@pytest.mark.parametrize("H,W,N", [(96, 80, 64), (128, 128, 200)])
+def test_device_loop_incremental_switched_on_mid_run_equals_full(H, W, N):
+    """a device loop run with incremental evaluation OFF accepts
+    neighbours without installing their records / strip partials, so switching it
+    ON afterwards must re-derive them (ggs_sa_set_incremental) before the dirty-
+    strip test relies on them.  Session A: 6 iterations full, then incremental on,
+    6 more; session B: full throughout, same seed and temperatures — identical
+    curves, current and best states, bit for bit.  Also on -> off -> on, and on
+    right after create (nothing to re-derive)."""
+    from ggs.ga_device import DeviceSA
+    target, t, m = _problem(H, W, 12)
+    init = ga.new_population(1, N, H, W, MIN_S, MAX_S, np.random.default_rng(N))[0]
+    temps = np.full(12, 5e-2)
+
+    def session(inc0):
+        return DeviceSA(t, m, init, max_tries=8, mutpb=0.05, min_scale_splats=MIN_S, max_scale_splats=MAX_S,
+                        seed=23, incremental=inc0, **CFG)
+
+    def drive(sa, plan):
+        curves = []
+        for (i0, i1), inc in plan:
+            if inc is not None:
+                ggs._lib.check(ggs._lib.lib.ggs_sa_set_incremental(sa.h, int(inc)), "set_incremental")
+            curves.append(sa.run(i0, temps[i0:i1], 12, 4))
+        cur, best, _ = sa.read()
+        sa.close()
+        return np.concatenate(curves), cur, best
+
+    full = drive(session(False), [((0, 12), None)])
+    for inc0, plan in ((False, [((0, 6), None), ((6, 12), True)]),
+                       (True, [((0, 4), None), ((4, 8), False), ((8, 12), True)]),
+                       (True, [((0, 12), None)])):
+        got = drive(session(inc0), plan)
+        for a, b in zip(got, full):
+            np.testing.assert_array_equal(a, b)
