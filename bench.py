@@ -74,7 +74,7 @@ METRIC = "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=
 GATHER = os.environ.get("GGS_BENCH_GATHER", "rccl")
 # Consecutive batches are independent populations, so they alternate over four
 # HIP streams: one batch's raster fills the CUs the others' grid tails (and their
-# prep/finalize launches) leave idle (781-786k vs 766-768k
+# prep/finalize launches) leave idle (docs/EXPERIMENTS.md §5: 781-786k vs 766-768k
 # renders/s at two streams, eight 763-768k).
 STREAMS = int(os.environ.get("GGS_BENCH_STREAMS", "4"))
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -759,7 +759,7 @@ def run(args, world, rank, local_rank, distributed):
         valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
         busy = pmc_valu_busy(prof_cfg) if profiled else None
         _, busy_src = _summary(prof_cfg) if profiled else (None, None)
-        # The raster is bound by the VALU (SURVEY.md §8d, DESIGN.md §3): `bound` names
+        # The raster is bound by the VALU (SURVEY.md §8d, DESIGN.md §4): `bound` names
         # that roof.  achieved / peak / frac are the HBM figures the contract defines
         # (algorithmic bytes per launch / HIP-event launch time vs 8 TB/s, frac_roof);
         # the VALU's executed-work fraction is binding_frac (PMC busy).

@@ -89,9 +89,14 @@ int ensure_zeroed(DevBuf& b, size_t bytes, hipStream_t st) {
     return GGS_OK;
 }
 
-// The fitness finalize runs inside the raster (FinFused: the last strip wave of
-// each candidate reduces it), saving a launch per evaluation; GGS_UNFUSED_FINALIZE=1
-// restores the separate finalize_kernel launch (A/B switch, same bits).
+// The device GA folds the fitness finalize into the raster (FinFused: the last
+// strip wave of each candidate reduces it): its generation is one breed and one
+// raster launch, and the launch the fold saves is worth more than the per-wave
+// count it adds (shipped run +1.3 %).  The fitness API keeps the separate
+// finalize launch: with four streams of independent batches the fold measured
+// -0.4 % and +17 MB of write traffic per launch, with one stream +0.1 %
+// (docs/EXPERIMENTS.md §14).  GGS_UNFUSED_FINALIZE=1 unfuses the GA too (A/B
+// switch, same bits).
 bool finalize_fused() {
     static const bool off = getenv("GGS_UNFUSED_FINALIZE") && atoi(getenv("GGS_UNFUSED_FINALIZE")) != 0;
     return !off;
@@ -203,10 +208,11 @@ void prof_drain_locked() {
     g_prof_pending.clear();
 }
 
-// raster (MODE 1) + finalize of B candidates: one launch when fused.
+// raster (MODE 1) + finalize of B candidates: one launch when `fuse` (and allowed).
 int raster_fitness(hipStream_t st, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                    const float4* plan, float* partials, const float* wpartials, int mode, const int* order,
-                   DevBuf& ctr, float* out, const unsigned char* dirty = nullptr, const float* clean = nullptr) {
+                   DevBuf& ctr, float* out, bool fuse, const unsigned char* dirty = nullptr,
+                   const float* clean = nullptr) {
     const float bg[3] = {1.f, 1.f, 1.f};  // fitness renders with the default background (fitness.py:15)
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
@@ -214,7 +220,7 @@ int raster_fitness(hipStream_t st, const SplatRec* recs, const int4* bnds, int B
     // a multiple of 32 floats: 512^2, 1024^2, 2048^2 ...): a line is then read, with
     // agent-scope loads, by one wave only, after every store to it, and never sits
     // in that XCD's L2 from an earlier read of a neighbour candidate's finalize
-    if (finalize_fused() && (4 * nTiles) % 32 == 0) {
+    if (fuse && finalize_fused() && (4 * nTiles) % 32 == 0) {
         int rc;
         if ((rc = ensure_zeroed(ctr, sizeof(int) * (size_t)std::max(B, 1), st))) return rc;
         FinFused ff;
@@ -406,7 +412,7 @@ int run_fitness_planned(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B
         GGS_HIP(launch_prep(st, true, d_gen, B * N, C, H, W, k, recs, (int4*)w->bnds.p, nullptr, nullptr, nullptr));
     }
     return raster_fitness(st, recs, (const int4*)w->bnds.p, (int)B, N, H, W, plan, (float*)w->partials.p,
-                          wpartials, mode, (const int*)w->order.p, w->fctr, d_out);
+                          wpartials, mode, (const int*)w->order.p, w->fctr, d_out, false);
 }
 
 int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, int C, int H, int W,
@@ -1149,7 +1155,7 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
                                        (const int4*)s->bnds.p + (int64_t)b0 * N, nb, N, c.H, c.W,
                                        (const float4*)s->plan.p, (float*)s->partials.p, (const float*)s->wpart.p,
                                        c.fitness_mode, (const int*)s->order.p, s->fctr,
-                                       (float*)s->off_fits.p + b0)))
+                                       (float*)s->off_fits.p + b0, true)))
         return rc;
     if (s->comm && per > 0) {   // one in-place all-gather of the shards' fitness scalars (RCCL, same stream)
         float* of = (float*)s->off_fits.p;
@@ -1170,7 +1176,7 @@ struct SaSession {
     hipStream_t st = nullptr;
     ggs_ga_config cfg{};
     int N = 0, cap = 0, last_n = 0, nTiles = 0;
-    bool incremental = false;   // measured slower at every SA config tried (DESIGN.md §9)
+    bool incremental = false;   // measured slower at every SA config tried (DESIGN.md §8)
     // cur_recs / cur_part describe the current state (create evaluates them, commit and
     // an incremental device run install them); a non-incremental ggs_sa_run may
     // accept neighbours without installing them
@@ -1213,7 +1219,7 @@ int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, int4* bnds, flo
         GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, G, (const SplatRec*)s->cur_recs.p, recs, n,
                              s->N, c.H, c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p));
     return raster_fitness(s->st, recs, bnds, n, s->N, c.H, c.W, (const float4*)s->plan.p, part,
-                          (const float*)s->wpart.p, c.fitness_mode, (const int*)s->order.p, s->fctr, fits,
+                          (const float*)s->wpart.p, c.fitness_mode, (const int*)s->order.p, s->fctr, fits, false,
                           dirty ? (const unsigned char*)s->dirty.p : nullptr, (const float*)s->cur_part.p);
 }
 
@@ -1682,7 +1688,7 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
     // A batch holds at most GGS_SA_MAX_ROUNDS_PER_SYNC rounds (ggs_sa_rounds_per_sync):
     // unbounded, a 256-iteration chunk at high acceptance queued ~1,000 rounds =
     // 4,000 dispatches behind one sync, and rocprofv3's PMC dispatch interception
-    // crashed the host thread inside the launch call.
+    // crashed the host thread inside the launch call (docs/EXPERIMENTS.md §9).
     const uint64_t evaluated0 = s->h_loop->evaluated;
     int64_t remaining = end - pos0;
     int est = gcap;

@@ -86,7 +86,7 @@ def simulated_annealing(target_img_uint8, H: int, W: int, device, n_splats: int,
     (bit-identical results; off by default — the double ``wrap_angle`` of
     genetic.py:71 + utils.py:43 moves many θ by an ulp on every mutation, so
     most strips are dirty anyway and the bookkeeping costs more than it saves,
-    DESIGN.md §9).  ``loop``: "device" (the whole iteration on the GPU, see the
+    DESIGN.md §8).  ``loop``: "device" (the whole iteration on the GPU, see the
     module doc; device backend, Philox draws), "host" (acceptance test in Python)
     or "auto" (device when possible).  ``chunk``: iterations per ``ggs_sa_run``
     call in the device loop (progress bar / interrupt granularity; video frames

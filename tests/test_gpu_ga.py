@@ -166,21 +166,59 @@ np.savez(sys.argv[2], population=st["population"], fitness=st["fitness"], best=s
 @pytest.mark.parametrize("P,N", [(128, 256), (32, 512)])
 def test_device_ga_fused_breed_equals_unfused(tmp_path, P, N):
     """The fused breed (survivors + gather inside the variation kernel) against the
-    five-launch generation (GGS_GA_UNFUSED=1) at the bench workload and at the
-    reference's shipped run (config.py: 512 splats, pop 32), 25 generations of
-    Philox draws in one run: identical populations, fitness, best and curves."""
+    five-launch generation (GGS_GA_UNFUSED=1), and the finalize folded into the
+    raster against its own launch (GGS_UNFUSED_FINALIZE=1), at the bench workload
+    and at the reference's shipped run (config.py: 512 splats, pop 32), 25
+    generations of Philox draws in one run: identical populations, fitness, best
+    and curves."""
     import os
     import subprocess
     import sys
     pkg = os.path.dirname(os.path.dirname(ggs.__file__))
     out = {}
-    for tag, env in (("fused", {}), ("unfused", {"GGS_GA_UNFUSED": "1"})):
+    for tag, env in (("fused", {}), ("unfused", {"GGS_GA_UNFUSED": "1"}),
+                     ("unfused_fin", {"GGS_UNFUSED_FINALIZE": "1"})):
         path = str(tmp_path / f"{tag}.npz")
         subprocess.run([sys.executable, "-c", _FUSED_SCRIPT, pkg, path, str(P), str(N)], check=True, timeout=300,
                        env=dict(os.environ, **env))
         out[tag] = np.load(path)
     for k in out["fused"].files:
         np.testing.assert_array_equal(out["fused"][k], out["unfused"][k], err_msg=k)
+        np.testing.assert_array_equal(out["fused"][k], out["unfused_fin"][k], err_msg=k)
+
+
+def test_device_ga_sessions_concurrent_uneven_load_equal_solo():
+    """Three device GA sessions of different shapes (each its own stream, its own
+    finalize counters) stepping at the same time from three threads — the raster's
+    folded finalize hands partials between waves on any XCD under uneven load —
+    end in exactly the state each reaches alone."""
+    import threading
+    shapes = [(512, 256, 128, 1), (512, 512, 32, 2), (1024, 1024, 8, 3)]
+
+    def run(H, N, P, seed):
+        target, t, m = _problem(H, H, seed)
+        init = ga.new_population(P, N, H, H, MIN_S, MAX_S, np.random.default_rng(seed))
+        dga = DeviceGA(t, m, init, tour_k=2, elite_k=min(8, P - 1), cxpb=0.05, mutpb=0.05,
+                       min_scale_splats=MIN_S, max_scale_splats=MAX_S, seed=seed, **CFG)
+        dga.run(1, 40, 40)
+        st = dga.read()
+        dga.close()
+        return st
+
+    solo = [run(*sh) for sh in shapes]
+    got = [None] * len(shapes)
+
+    def worker(i):
+        got[i] = run(*shapes[i])
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(shapes))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(300)
+    for a, b in zip(got, solo):
+        np.testing.assert_array_equal(a["population"], b["population"])
+        np.testing.assert_array_equal(a["fitness"], b["fitness"])
+        assert a["best_fit"] == b["best_fit"]
 
 
 def test_device_ga_read_is_idempotent_and_resumable():

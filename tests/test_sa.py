@@ -126,7 +126,7 @@ def test_device_loop_batching_rule_is_bounded():
     arithmetic): enough rounds to finish the chunk at the expected consumption
     (never past it), at least one, and never more than GGS_SA_MAX_ROUNDS_PER_SYNC
     — an unbounded batch (~1,000 rounds = 4,000 queued dispatches at high
-    acceptance) crashed the launch under rocprofv3 --pmc."""
+    acceptance) crashed the launch under rocprofv3 --pmc (docs/EXPERIMENTS.md §9)."""
     import re
     from conftest import REPO
     from ggs import lib

@@ -1,7 +1,7 @@
 """Probe: does rocprofv3 --pmc survive K fitness evaluations (3 dispatches each)
 enqueued behind ONE host sync?  Tiny workload (64^2, 8 splats, 4 candidates), so
 only the number of queued dispatches varies.  Used to establish the cause of the
-round-2 SIGSEGV in ggs_sa_run under --pmc.
+round-2 SIGSEGV in ggs_sa_run under --pmc (docs/EXPERIMENTS.md §9).
 
     rocprofv3 --pmc FETCH_SIZE -- python3 tools/probe/queue_depth_pmc.py K
 """

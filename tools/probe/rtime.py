@@ -17,7 +17,8 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-CFG = {"512": (512, 256, 128), "1024": (1024, 1024, 512), "1024x8": (1024, 1024, 4096), "sa16": (2048, 4096, 16), "sa2": (2048, 4096, 2)}
+CFG = {"512": (512, 256, 128), "1024": (1024, 1024, 512), "1024x8": (1024, 1024, 4096), "sa16": (2048, 4096, 16),
+       "sa2": (2048, 4096, 2), "ga24": (512, 512, 24)}   # ga24: the shipped GA run's launch (config.py)
 
 
 def worker(cfg, steps, out_npy):
@@ -70,7 +71,7 @@ def main():
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    steps = a.steps or {"512": 300, "1024": 20, "1024x8": 4, "sa16": 60, "sa2": 200}[a.config]
+    steps = a.steps or {"512": 300, "1024": 20, "1024x8": 4, "sa16": 60, "sa2": 200, "ga24": 600}[a.config]
     if a.worker:
         worker(a.config, steps, a.out)
         return
