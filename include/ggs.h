@@ -131,9 +131,11 @@ void ggs_plan_destroy(void* plan);
  * population, fitness, elites, best individual and curves stay in HBM; a
  * generation is variation -> fitness -> survivors -> gather, no host sync.
  * Up to pop_size 512 the survivors/gather of a generation run inside the next
- * generation's variation launch ("breed": 3 launches per generation instead of
- * 5); ggs_ga_read applies the last generation's first, so what it returns is the
- * same either way (GGS_GA_UNFUSED=1 in the environment: always 5 launches).
+ * generation's variation launch ("breed"), and the fitness finalize inside the
+ * raster launch (its last strip wave per candidate reduces): 2 launches per
+ * generation instead of 5; ggs_ga_read applies the last generation's survivors
+ * first, so what it returns is the same either way (GGS_GA_UNFUSED=1: separate
+ * survivors/gather launches; GGS_UNFUSED_FINALIZE=1: a separate finalize launch).
  * Draws: explicit arrays (ggs_ga_step with draws != NULL; replay / parity) or a
  * counter-based Philox4x32-10 stream keyed by (seed, generation, individual). */
 typedef struct ggs_ga_config {
@@ -276,7 +278,8 @@ int ggs_comm_barrier(void* comm);
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------
  * When enabled, every launch of "prep", "raster" and "finalize" is bracketed
  * by hipEvents; ggs_profile_read synchronises those events and returns the
- * accumulated milliseconds and launch count for the named kernel. */
+ * accumulated milliseconds and launch count for the named kernel (a finalize
+ * folded into the raster counts as raster time, no finalize launch). */
 int ggs_profile_enable(int32_t on);
 int ggs_profile_read(const char* kernel, double* total_ms, int64_t* launches);
 void ggs_profile_reset(void);
