@@ -1,8 +1,8 @@
 """Per-workgroup phase clocks of the GA's variation / breed kernel (diagnostic
 build GGS_VTIMING=1; thread 0's s_memrealtime, 100 MHz, at each phase boundary).
 
-    make -C genetic-gaussian-splats_amd/csrc OUT=../libggs_vt.so BUILD=build_vt EXTRA=-DGGS_VTIMING=1
-    GGS_LIB=genetic-gaussian-splats_amd/libggs_vt.so python tools/probe/breed_timing.py
+    make -C genetic-gaussian-splats_amd/csrc probe PROBE="-DGGS_TIMING=1 -DGGS_VTIMING=1"
+    GGS_PROBE=1 GGS_LIB=genetic-gaussian-splats_amd/libggs_probe.so [P=32 N=512] python tools/probe/breed_timing.py
 
 Runs 30 device-GA generations at the bench workload (512^2, 256 splats, pop 128)
 and prints, for the last launch, the median/max time of each phase over the
