@@ -96,6 +96,20 @@ def test_bench_world2_orchestration(tmp_path):
     assert not (tmp_path / "stdout1.txt").read_text().strip()               # rank 1 prints nothing
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_world_n_orchestration(tmp_path, world):
+    """The same control flow at the driver's larger worlds: every rank makes its
+    four communicators from the same ids, issues the same collectives, and rank 0
+    alone prints one line with n_gpus = world and global_batch = 128 * world."""
+    codes, logs, out0 = _run_world(tmp_path, ["--gpus", str(world)] + FAST, world=world)
+    assert codes == [0] * world, logs
+    assert all(lg["comms"] == logs[0]["comms"] and lg["gathers"] == logs[0]["gathers"] for lg in logs)
+    assert [lg["device"] for lg in logs] == list(range(world))
+    line = json.loads(out0[0])
+    assert line["n_gpus"] == world and line["config"]["global_batch"] == 128 * world
+    assert line["config"]["rccl_ranks"] == world and len(out0) == 1
+
+
 def test_bench_world2_strong_scaling_splits_configs3(tmp_path):
     """--config 1024x8 (configs[3]): one population of 4096 split 2048 per rank,
     2048 fitness scalars per rank in each gather, global_batch 4096."""
