@@ -145,10 +145,14 @@ constexpr int SAT_BATCH = GGS_SAT_BATCH;
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// One strip's partial (lane 0): an agent-scope store, written through to the
-// device coherence point, where a fused finalize on another XCD reads it.
-__device__ __forceinline__ void store_partial(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// One strip's partial (lane 0).  With the fused finalize: an agent-scope store,
+// written through to the device coherence point, where the candidate's last wave
+// (on any XCD) reads it.  Otherwise a plain store (the finalize launch reads it
+// after the kernel boundary): the write-through store of every wave measured
+// 16 MB of extra write traffic per 512^2 launch (PMC WRITE_SIZE, 0.45 MB plain).
+__device__ __forceinline__ void store_partial(float* p, float v, bool fused) {
+    if (fused) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
 }
 // The fused finalize (FinFused), after lane 0 stored this strip's partial.  The
 // partial is the only data another wave reads, and its agent-scope store is
@@ -329,7 +333,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     if (MODE != 0 && dirty) {         // incremental (SA): a strip no changed splat touches
         const int64_t slot = ((int64_t)b * nTiles + t) * 4 + wv;   // keeps the current state's
         if (!dirty[slot]) {                                         // partial, bit for bit
-            if (lane == 0) store_partial(partials + slot, clean[t * 4 + wv]);
+            if (lane == 0) store_partial(partials + slot, clean[t * 4 + wv], fin.ctr != nullptr);
             if (fin.ctr) strip_done(fin, partials, b, nTiles * 4, lane);
             return;
         }
@@ -696,7 +700,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if (lane == 0)        // one partial per (candidate, tile, strip): no block barrier
-            store_partial(partials + ((int64_t)b * nTiles + t) * 4 + wv, acc);
+            store_partial(partials + ((int64_t)b * nTiles + t) * 4 + wv, acc, fin.ctr != nullptr);
         if (fin.ctr) strip_done(fin, partials, b, nTiles * 4, lane);
     }
 #if GGS_TIMING
