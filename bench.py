@@ -65,7 +65,7 @@ K_SIGMA = 3.0
 N_POPS = 4
 RING = 8                         # in-flight fitness vectors (gather overlap)
 METRIC = "candidate renders/sec (and Gsplat-pixels/s), 512x512, 256 splats, pop=128"
-# How the per-step fitness all-gather is issued (A/B switch, tools/gather_exp.sh):
+# How the per-step fitness all-gather is issued (A/B switch; docs/EXPERIMENTS.md §5):
 #   "rccl"          (default) libggs's RCCL communicator, in order on the compute
 #                   stream right after finalize: +1.5 us per step at world 1
 #   "rccl-overlap"  the same on the communicator's own stream, joined through the

@@ -107,7 +107,7 @@ constexpr int XCD_SHIFT = 3;
 constexpr int CULL_PRIO = 2;      // s_setprio while culling (1 and 3 measured the same)
 
 #ifndef GGS_NOPLAN
-#define GGS_NOPLAN 0      // diagnostic build (tools/probe/traffic_ab.sh): the epilogue reads no plan
+#define GGS_NOPLAN 0      // probe build only (docs/EXPERIMENTS.md §4 traffic split): the epilogue reads no plan
 #endif
 
 // Saturation cut-off.  Front to back, a strip's pixels receive Σ_rest T·f·c +
