@@ -359,9 +359,10 @@ class Watchdog:
 
     # ---- watchdog thread ---------------------------------------------------------------
     def state(self) -> dict:
+        issued = dict(self.issued)          # one C-level copy: the main thread may add a key
         return {"rank": self.rank, "phase": self.phase, "step": self.step, "stream": self.stream,
-                "issued": {str(k): v for k, v in sorted(self.issued.items())},
-                "issued_total": sum(self.issued.values()), "last_ticket": self.last_ticket,
+                "issued": {str(k): v for k, v in sorted(issued.items())},
+                "issued_total": sum(issued.values()), "last_ticket": self.last_ticket,
                 "in_phase_s": round(time.monotonic() - self.t_arm, 3), "wall": time.time()}
 
     def _write(self) -> None:
@@ -375,7 +376,10 @@ class Watchdog:
 
     def _run(self) -> None:
         while not self._stop.wait(self.period):
-            self._write()
+            try:
+                self._write()
+            except Exception:  # noqa: BLE001 — a heartbeat write never stops the watchdog
+                pass
             d = self.deadline
             if d is not None and time.monotonic() > d:
                 self._expire()
