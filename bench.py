@@ -767,8 +767,8 @@ def run(args, world, rank, local_rank, distributed):
         # that roof.  achieved / peak / frac are the HBM figures the contract defines
         # (algorithmic bytes per launch / HIP-event launch time vs 8 TB/s, frac_roof);
         # the VALU's executed-work fraction is binding_frac (PMC busy).
-        roof = {"bound": "valu", "kernel": "raster_kernel<1, false>" if N_SPLATS <= 512 else
-                "raster_kernel<1, true>",
+        roof = {"bound": "valu", "kernel": "raster_kernel<1, false, false>" if N_SPLATS <= 512 else
+                "raster_kernel<1, true, false>",
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "frac_roof": "hbm",
                 "traffic": None if traffic is None else round(traffic),

@@ -29,13 +29,17 @@ namespace ggs {
 // r, g, b: colour in [0,1] (render.py:40-42); x0..y1: inclusive integer AABB
 // (render.py:27-30).
 struct __attribute__((aligned(16))) SplatRec {
-    // Cc, r, g, b, rho and c16 sit in EVEN dwords: a 16-dword s_load lands them in
+    // C64, r, g, b and rho sit in EVEN dwords: a 16-dword s_load lands them in
     // even SGPRs, the low half of an aligned SGPR pair, which the raster's v_pk_*
     // ops broadcast to both halves (op_sel_hi) with no per-visit copy (round 3:
     // raster -2.8 % vs odd dwords, which the compiler copied into even SGPRs).
-    float Cc, cx, r, cy;
-    float g, A, b, Bc;
-    float rho, la, c16, rho4;  // row-recurrence constants: 2^(128 Cc), 16 Cc, 2^(64 Cc) (8-row step)
+    // (A, B8) is one aligned pair: one v_pk_mul forms (A qx, 8 Bc qx) per visit.
+    // The raster works with qy / 8 (cy8): C64 = 64 Cc, B8 = 8 Bc and c128 = 128 Cc
+    // are the exponent's y-terms rescaled by powers of two (exact), so the
+    // recurrence ratio needs no separate 8 * bx (see make_rec).
+    float C64, cx, r, cy8;
+    float g, la, b, c128;
+    float rho, rho4, A, B8;    // row-recurrence constants: 2^(128 Cc), 2^(64 Cc) (8-row step)
     int x0, x1, y0, y1;
 };
 static_assert(sizeof(SplatRec) == 64, "SplatRec must be 64 bytes");

@@ -98,7 +98,7 @@ constexpr int SPB = 4 / WPB;      // workgroups per (candidate, tile)
 constexpr int CAP = 1024;         // LDS list capacity per wave (splats per cull round)
 constexpr int OCC = 3;            // waves per SIMD the register budget is sized for (<= 168 VGPRs)
 // candidate rotation across the XCDs advances every 2^XCD_SHIFT strip groups (see the grid order)
-// (launches with N > SAT_MIN_SPLATS, the raster_kernel<M, true> instances; the others
+// (launches with N > SAT_MIN_SPLATS, the raster_kernel<M, true, F> instances; the others
 // rotate every group: at 512^2/256 splats the whole launch's records (2.1 MB) and the
 // 4-MiB target plan share each XCD's L2, and rotating every group lets each XCD read
 // each strip's plan slice once: 54 vs 80 MB of fabric traffic per launch, raster
@@ -221,7 +221,7 @@ typedef float f2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_elementwise_fma(a, b, c); }
 #define GGS_PK(k, MASKED)                                                            \
     do {                                                                             \
-        const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                   \
+        const f2_t qy_ = (k) == 0 ? qyv : qyv + (f2_t)(float)(k);  /* no +0 add */    \
         f2_t e_ = GGS_E1(qy_);                                                       \
         if (MASKED) {                                                                \
             if ((unsigned)(8 * (k) - rlo) > rspan) e_.x = -__builtin_inff();         \
@@ -251,22 +251,28 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
         R2 = R2 * (f2_t)s.rho;                                                       \
         GGS_BLEND(k, F2);                                                            \
     }
-// The first pair's ratio to the next: 2^d, d(qy) = 16 Cc (qy + 4) + 8 bx.  Live
-// lanes have d <= -e(seed) <= 100 (make_rec's seed guard: e <= 0 everywhere), so
-// the clamp is exact there; dead lanes (px = -inf, f = 0) only need a finite
-// ratio (0 * r = 0), which the clamp gives without a per-lane select (round 3:
-// raster -1.0 %, bit-identical).
-#define GGS_RATIO(qy) GGS_EXP2(fminf(__builtin_fmaf((qy), s.c16, 8.0f * bx), 100.0f))
-// The first pair's exponent e = qy (Cc qy + bx) + px for both rows of the pair.
-// Cc broadcast from the low half of the record's (Cc, cx) SGPR pair and bx, px
-// from the low half of VGPR pairs whose high half is never set (op_sel_hi 0): no
-// per-visit broadcast copies of bx and px (LLVM copies a splat of a VGPR into a pair
-// of its own; round 3: raster -0.2 % at 512^2, -0.5 % at 1024^2, bit-identical)
+// The first pair's ratio to the next: 2^d, d(qy) = 16 Cc (qy + 4) + 8 bx, in the
+// record's scaled terms fma((qy + 4)/8, 128 Cc, 8 bx) (the .y row's qy/8).  Live
+// lanes of well-formed splats have d <= -e(seed) <= 100 (make_rec's seed guard:
+// e <= 0 everywhere), so the clamp is exact there; lanes with f = 0 (outside the
+// AABB's columns, or a degenerate splat's: infinite conic terms) only need a
+// finite ratio (0 * r = 0), which the clamp gives without a per-lane select
+// (round 3: raster -1.0 %, bit-identical).  (Round 4 measured the clamp's
+// removal with 8 bx = -1e30 on the column-clipped lanes: raster -0.3 %, but the
+// configs[4] SA trajectory changed, so some state's splats rely on it.)
+#define GGS_RATIO(qy8) GGS_EXP2(fminf(__builtin_fmaf((qy8), s.c128, abx.y), 100.0f))
+// The first pair's exponent e = qy (Cc qy + bx) + px for both rows of the pair,
+// as (qy/8) (64 Cc (qy/8) + 8 bx) + px (make_rec: the same bits).  64 Cc broadcast
+// from the low half of the record's (C64, cx) SGPR pair, 8 bx from the high half
+// of abx = (A qx, 8 Bc qx) and px from the low half of a VGPR pair whose
+// high half is never set: no per-visit broadcast copies (LLVM copies a splat of a
+// VGPR into a pair of its own; round 3: raster -0.2 % at 512^2, -0.5 % at 1024^2,
+// bit-identical)
 #define GGS_E1(qy) ({                                                                     \
-        f2_t t_, e2_, bxu_, pxu_;                                                         \
-        bxu_.x = bx; pxu_.x = px;                                                         \
-        const uint64_t ccp_ = *reinterpret_cast<const uint64_t*>(&s.Cc);                  \
-        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(t_) : "s"(ccp_), "v"(qy), "v"(bxu_)); \
+        f2_t t_, e2_, pxu_;                                                               \
+        pxu_.x = px;                                                                      \
+        const uint64_t ccp_ = *reinterpret_cast<const uint64_t*>(&s.C64);                  \
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[0,1,1]" : "=v"(t_) : "s"(ccp_), "v"(qy), "v"(abx)); \
         asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(e2_) : "v"(qy), "v"(t_), "v"(pxu_)); \
         e2_; })
 #define GGS_FOR8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
@@ -280,7 +286,7 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 // per step, highest index first, ballot + mbcnt compaction -> an order-
 // preserving LDS list), blends that list front-to-back, and writes its own
 // partial sum.  TILE_H = 128: 128 accumulator VGPRs (+~35) -> 3 waves per SIMD.
-template <int MODE, bool SAT>
+template <int MODE, bool SAT, bool FUSED>
 __global__ void __launch_bounds__(NT, OCC)
 raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, int B, int N, int H, int W, int nTX,
               int nTiles,
@@ -333,8 +339,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     if (MODE != 0 && dirty) {         // incremental (SA): a strip no changed splat touches
         const int64_t slot = ((int64_t)b * nTiles + t) * 4 + wv;   // keeps the current state's
         if (!dirty[slot]) {                                         // partial, bit for bit
-            if (lane == 0) store_partial(partials + slot, clean[t * 4 + wv], fin.ctr != nullptr);
-            if (fin.ctr) strip_done(fin, partials, b, nTiles * 4, lane);
+            if (lane == 0) store_partial(partials + slot, clean[t * 4 + wv], FUSED);
+            if (FUSED) strip_done(fin, partials, b, nTiles * 4, lane);
             return;
         }
     }
@@ -346,7 +352,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     const float Yb = (float)(ty0 + ph);
     // the lane's two rows of pair 0: a visit's first-pair offsets qy are one packed
     // subtract (round 3: -1.0 % raster vs qy0 then qy0 + 4)
-    const f2_t Ybv = {Yb, Yb + 4.0f};
+    const f2_t Ybv = {0.125f * Yb, 0.125f * (Yb + 4.0f)};   // in eighths (see make_rec)
 
     // 16 pixels per lane x (R, G, B, transmittance), as named scalars: arrays
     // get vectorised into <16 x float> values whose phis the allocator splits.
@@ -444,14 +450,28 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             const int gA = max(dy0, 0) >> 2;                   // first / last row group
             const int gB = min(dy1, TILE_H - 1) >> 2;
             const float qx = Xf - s.cx;
-            const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
-            const float px = inx ? __builtin_fmaf(s.A * qx, qx, s.la) : -__builtin_inff();
-            const float bx = s.Bc * qx;
-            const f2_t qyv = Ybv - (f2_t)s.cy;
+            f2_t abx;                          // (A qx, Bc qx): one v_pk_mul from the (A, Bc) pair
+            abx.x = s.A * qx;
+            abx.y = s.B8 * qx;
+            float px = __builtin_fmaf(abx.x, qx, s.la);
+            // the AABB's column clip: only when it cuts the strip's 16 columns (a
+            // wave-uniform branch; 85 % of the bench's visits span all 16 columns.
+            // The empty asm keeps the compiler from if-converting it back into an
+            // unconditional compare + select).  Dead lanes: px = -inf (f = 0; the
+            // ratio's clamp keeps their walk at 0, see GGS_RATIO).
+            if (max(x0 - sx0, sx0 + 15 - x1) > 0) {
+                const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
+                px = inx ? px : -__builtin_inff();
+                asm volatile("" : "+v"(px));
+            }
+            const f2_t qyv = Ybv - (f2_t)s.cy8;          // qy / 8 of the lane's rows
             const int rlo = y0 - ty0 - ph;                     // row test: 4g - rlo in [0, rspan]
             const unsigned rspan = (unsigned)(y1 - y0);
 
-            const int kA = gA >> 1, kB = gB >> 1;             // first / last group pair
+            // first / last group pair; kB = NPK: the splat reaches past the tile's
+            // last row, so the walk's last pair needs no bottom-row mask (about half
+            // the partial visits: 4 VALU fewer each, the same bits)
+            const int kA = gA >> 1, kB = dy1 >= TILE_H - 1 ? NPK : gB >> 1;
             f2_t F2, R2;                                       // row recurrence: f, ratio
             // First pair: exact exponent; keeps the unmasked f as the recurrence
             // seed and, when more pairs follow, the ratio 2^d to the next pair.
@@ -487,15 +507,38 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #undef GGS_FULL
                 goto done;
             }
-            // about half the partial visits start at the tile's top (the splat began
-            // in a tile above): test that before the switch's compare tree
+            // About half the partial visits start above the tile (the splat began in
+            // a tile above): their first pair needs no top-row mask (GGS_FIRST(0)
+            // with all-ones masks: the same bits, 4 VALU fewer).
+            if (dy0 <= 0) {
+                const f2_t e_ = GGS_E1(qyv);
+                F2.x = GGS_EXP2(e_.x);
+                F2.y = GGS_EXP2(e_.y);
+                if (kB == 0) {                                 // one pair: bottom limit only
+                    const PairLanes bot_ = rows_upto(dy1);
+                    f2_t fu_;
+                    fu_.x = keep_if(bot_.x, F2.x);
+                    fu_.y = keep_if(bot_.y, F2.y);
+                    GGS_BLEND(0, fu_);
+                    goto done;
+                }
+                GGS_BLEND(0, F2);
+                if ((__float_as_uint(s.rho4) >> 31) &&
+                    __ballot((px > -__builtin_inff()) &
+                             (min(__float_as_uint(F2.x), __float_as_uint(F2.y)) < 0x0D800000u)))
+                    goto x0;
+                R2.x = GGS_RATIO(qyv.y);
+                R2.y = R2.x * __builtin_fabsf(s.rho4);
+                goto u0;
+            }
+            // the rest of the visits starting in pair 0: before the switch's compare tree
             if (kA == 0) goto f0;
             switch (kA) {
 #define GGS_FIRST(k)                                                                    \
     case k:                                                                             \
     f##k: __attribute__((unused));                                                      \
         if (k < NPK) {                                                                  \
-            const f2_t qy_ = qyv + (f2_t)(8.0f * (k));                                  \
+            const f2_t qy_ = (k) == 0 ? qyv : qyv + (f2_t)(float)(k);                   \
             const f2_t e_ = GGS_E1(qy_);                                                \
             F2.x = GGS_EXP2(e_.x);                                                      \
             F2.y = GGS_EXP2(e_.y);                                                      \
@@ -545,10 +588,21 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         fu_.y = keep_if(bot_.y, fr_.y);                                                 \
         GGS_BLEND(k, fu_);                                                              \
     }
+// the tile's last pair when the splat reaches past it (kB == NPK): no mask
+#define GGS_LASTF(k)                                                                    \
+    if ((k) < NPK) {                                                                    \
+        F2 = F2 * R2;                                                                   \
+        GGS_BLEND(k, F2);                                                               \
+    }
 #define GGS_MID3(k, k1, k2, k3)                                                         \
     u##k:                                                                               \
         if (kB > (k3)) {                                                                \
-            GGS_BLEND_REC(k1) GGS_BLEND_REC(k2) GGS_BLEND_REC(k3)                       \
+            GGS_BLEND_REC(k1) GGS_BLEND_REC(k2)                                         \
+            if ((k3) == NPK - 1) {                                                      \
+                GGS_LASTF(k3)                                                           \
+                goto done;                                                              \
+            }                                                                           \
+            GGS_BLEND_REC(k3)                                                           \
             goto u##k3;                                                                 \
         }                                                                               \
         if (kB == (k3)) {                                                               \
@@ -569,6 +623,11 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             GGS_MID3(11, 12, 13, 14) GGS_MID3(12, 13, 14, 15)
 #undef GGS_MID3
         u13:                          // pairs 14 and 15 are the last ones there are
+            if (kB == NPK) {
+                GGS_BLEND_REC(14)
+                GGS_LASTF(15)
+                goto done;
+            }
             if (kB == 15) {
                 GGS_BLEND_REC(14)
                 GGS_LASTB(15)
@@ -577,9 +636,14 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             GGS_LASTB(14)
             goto done;
         u14:
+            if (kB == NPK) {
+                GGS_LASTF(15)
+                goto done;
+            }
             GGS_LASTB(15)
             goto done;
 #undef GGS_LASTB
+#undef GGS_LASTF
         u15:
             goto done;
             // exact walk (guard tripped): the exponent per pair as before
@@ -596,6 +660,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
                 GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
                 GGS_LAST(7) GGS_LAST(8) GGS_LAST(9) GGS_LAST(10) GGS_LAST(11) GGS_LAST(12)
                 GGS_LAST(13) GGS_LAST(14) GGS_LAST(15)
+                case NPK: break;              // pair 15 ran unmasked (x14)
 #undef GGS_LAST
                 default: __builtin_unreachable();
             }
@@ -700,8 +765,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
         if (lane == 0)        // one partial per (candidate, tile, strip): no block barrier
-            store_partial(partials + ((int64_t)b * nTiles + t) * 4 + wv, acc, fin.ctr != nullptr);
-        if (fin.ctr) strip_done(fin, partials, b, nTiles * 4, lane);
+            store_partial(partials + ((int64_t)b * nTiles + t) * 4 + wv, acc, FUSED);
+        if (FUSED) strip_done(fin, partials, b, nTiles * 4, lane);
     }
 #if GGS_TIMING
     {
@@ -946,14 +1011,17 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const i
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
     const int CH = raster_chunk(N);
     const FinFused ff = (mode != 0 && fin) ? *fin : FinFused{};
-#define GGS_RASTER(M, S)                                                                       \
-    hipLaunchKernelGGL((raster_kernel<M, S>), grid, block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
+    // FUSED is a template parameter, so the instances without the fold carry none
+    // of its code (a runtime test left the SA raster 1 % slower than round 3's)
+#define GGS_RASTER(M, S, F)                                                                    \
+    hipLaunchKernelGGL((raster_kernel<M, S, F>), grid, block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
                        bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH, ff)
     // the saturation check only where strip lists can grow long (N > SAT_MIN_SPLATS);
     // at the bench's 256 splats the kernel without it is the faster code (+1.6 %)
     const bool sat = N > SAT_MIN_SPLATS;
-    if (mode == 0) { if (!sat) GGS_RASTER(0, false); else GGS_RASTER(0, true); }   // image
-    else { if (!sat) GGS_RASTER(1, false); else GGS_RASTER(1, true); }             // fitness (mode in the plan)
+    if (mode == 0) { if (!sat) GGS_RASTER(0, false, false); else GGS_RASTER(0, true, false); }   // image
+    else if (!ff.ctr) { if (!sat) GGS_RASTER(1, false, false); else GGS_RASTER(1, true, false); }   // fitness
+    else { if (!sat) GGS_RASTER(1, false, true); else GGS_RASTER(1, true, true); }  // + folded finalize
 #undef GGS_RASTER
     return hipGetLastError();
 }

@@ -84,10 +84,15 @@ __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
     constexpr float K = -0.72134752044448170f;
     SplatRec r;
     r.cx = p.cx;
-    r.cy = p.cy;
     r.A = K * p.sxx;
-    r.Bc = 2.0f * K * p.sxy;
-    r.Cc = K * p.syy;
+    const float Bc = 2.0f * K * p.sxy, Cc = K * p.syy;
+    // the raster's y-side in qy / 8: e = (qy/8) (64 Cc (qy/8) + 8 Bc qx) + px is
+    // e = qy (Cc qy + Bc qx) + px with every operand scaled by a power of two, so
+    // every rounding is the same (the same bits), and the row ratio's exponent
+    // d = 16 Cc (qy + 4) + 8 Bc qx is one FMA, 128 Cc (qy + 4)/8 + 8 Bc qx
+    r.cy8 = 0.125f * p.cy;
+    r.B8 = 8.0f * Bc;
+    r.C64 = 64.0f * Cc;
     r.la = p.a > 0.0f ? __builtin_amdgcn_logf(p.a) : -__builtin_inff();
     r.r = p.rc;
     r.g = p.gc;
@@ -95,9 +100,9 @@ __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
     // f(qy + 8) = f(qy) * 2^d(qy),  d(qy) = e(qy + 8) - e(qy) = 16 Cc (qy + 4) + 8 bx,
     // d(qy + 8) = d(qy) + 128 Cc  ->  the raster walks rows with two multiplies;
     // d(qy + 4) = d(qy) + 64 Cc   ->  the pair's second row ratio is one multiply.
-    r.rho = __builtin_amdgcn_exp2f(128.0f * r.Cc);
-    r.c16 = 16.0f * r.Cc;
-    r.rho4 = __builtin_amdgcn_exp2f(64.0f * r.Cc);
+    r.rho = __builtin_amdgcn_exp2f(128.0f * Cc);
+    r.c128 = 128.0f * Cc;
+    r.rho4 = __builtin_amdgcn_exp2f(64.0f * Cc);
     r.x0 = p.x0;
     r.x1 = p.x1;
     r.y0 = p.y0;
@@ -114,8 +119,8 @@ __device__ __forceinline__ SplatRec make_rec(const Prep13& p) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const float qx = (float)((c & 1) ? p.x1 : p.x0) - r.cx;
-        const float qy = (float)((c & 2) ? p.y1 : p.y0 - 7) - r.cy;
-        const float e = qy * (r.Cc * qy + r.Bc * qx) + (r.A * qx * qx + r.la);
+        const float qy = (float)((c & 2) ? p.y1 : p.y0 - 7) - p.cy;
+        const float e = qy * (Cc * qy + Bc * qx) + (r.A * qx * qx + r.la);
         emin = fminf(emin, e);
     }
     if (!(emin >= -99.0f)) r.rho4 = -r.rho4;     // NaN too
