@@ -450,7 +450,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             const int gA = max(dy0, 0) >> 2;                   // first / last row group
             const int gB = min(dy1, TILE_H - 1) >> 2;
             const float qx = Xf - s.cx;
-            f2_t abx;                          // (A qx, Bc qx): one v_pk_mul from the (A, Bc) pair
+            f2_t abx;                          // (A qx, 8 Bc qx): one v_pk_mul from the (A, B8) pair
             abx.x = s.A * qx;
             abx.y = s.B8 * qx;
             float px = __builtin_fmaf(abx.x, qx, s.la);
