@@ -587,6 +587,11 @@ def run(args, world, rank, local_rank, distributed):
     t_step = [None]
 
     def arm(phase, n_steps=0, extra_s=0.0):
+        if n_steps and t_step[0] is None:
+            # no step time measured yet (--ramp-ms 0): nothing to scale the deadline
+            # from, so the set-up's generous deadline applies instead of the bare floor
+            wd.arm(phase, max(args.watchdog_init_s, args.watchdog_floor_s + 20.0 * extra_s))
+            return
         est = (t_step[0] or 0.0) * n_steps + extra_s
         wd.arm(phase, args.watchdog_floor_s + 20.0 * est)
 
@@ -845,8 +850,11 @@ def run(args, world, rank, local_rank, distributed):
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    # communicator teardown can hang too (an RCCL destroy waits for its peers)
+    wd.arm("teardown (communicators)", args.watchdog_floor_s)
     for c in comms or ():
         c.close()
+    wd.disarm()
     wd.close()
 
 

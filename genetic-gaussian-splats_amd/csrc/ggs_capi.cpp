@@ -101,6 +101,13 @@ bool finalize_fused() {
     static const bool off = getenv("GGS_UNFUSED_FINALIZE") && atoi(getenv("GGS_UNFUSED_FINALIZE")) != 0;
     return !off;
 }
+// Test switch: GGS_FITNESS_FOLD=1 folds the finalize into the fitness API's raster
+// too (read per call, so one test process can cover both paths; the GA's fold
+// under concurrent, uneven load is otherwise exercised only through GA sessions).
+bool fitness_api_fold() {
+    const char* v = getenv("GGS_FITNESS_FOLD");
+    return v && atoi(v) != 0;
+}
 
 struct PinBuf {
     void* p = nullptr;
@@ -412,7 +419,7 @@ int run_fitness_planned(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B
         GGS_HIP(launch_prep(st, true, d_gen, B * N, C, H, W, k, recs, (int4*)w->bnds.p, nullptr, nullptr, nullptr));
     }
     return raster_fitness(st, recs, (const int4*)w->bnds.p, (int)B, N, H, W, plan, (float*)w->partials.p,
-                          wpartials, mode, (const int*)w->order.p, w->fctr, d_out, false);
+                          wpartials, mode, (const int*)w->order.p, w->fctr, d_out, fitness_api_fold());
 }
 
 int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, int C, int H, int W,

@@ -19,6 +19,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -104,6 +107,43 @@ struct Comm {
     float* scratch = nullptr;            // barrier / host all-gather staging (device)
     int64_t scratch_cap = 0;             // floats
     std::mutex mu;
+    std::shared_ptr<struct Loop> loop;   // loopback group (ggs_comm_init_loopback), no RCCL
+};
+
+// Loopback group: n communicators on ONE device in one process that act as
+// ranks 0..n-1 of one job, so the sharded paths (rank != 0, uneven and empty
+// shards, the fingerprint exchange) run on a one-GPU box.  Device all-gathers
+// are matched by sequence number: each rank's call records an event after the
+// work already on its stream (the producer of its send buffer) and returns;
+// the LAST rank's call enqueues, on every rank's stream, the waits on the
+// others' events and the device-to-device copies of their shards, then joins
+// the streams again (every stream waits for every copy), so no rank's later
+// work rewrites a shard another rank has still to read.  A rank that calls
+// again before every rank called fails (loopback ranks run in lockstep).
+// Host all-gathers are a blocking rendezvous (ranks on separate host threads),
+// bounded by GGS_LOOPBACK_TIMEOUT_S (default 60 s): a missing rank fails loudly.
+struct Loop {
+    int n = 1, dev = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    // device gathers
+    int64_t seq = 0;                     // the gather being collected
+    int arrived = 0;
+    std::vector<char> have;
+    std::vector<hipStream_t> st;
+    std::vector<const float*> send;
+    std::vector<float*> recv;
+    std::vector<int64_t> count;
+    std::vector<hipEvent_t> ev, done;
+    // host gathers
+    int64_t hgen = 0;
+    int harrived = 0;
+    int64_t hcount = -1;
+    std::vector<float> hbuf, hres;
+    ~Loop() {
+        for (auto e : ev) if (e) (void)hipEventDestroy(e);
+        for (auto e : done) if (e) (void)hipEventDestroy(e);
+    }
 };
 
 // Staging for the host-pointer collectives: [count | nranks*count] floats.
@@ -152,6 +192,73 @@ struct DevScope {
     ~DevScope() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
+int loop_allgather(Comm* c, hipStream_t stream, const float* d_send, float* d_recv, int64_t count) {
+    Loop& L = *c->loop;
+    std::lock_guard<std::mutex> lk(L.mu);
+    const int r = c->rank;
+    if (L.have[r])
+        return cfail(GGS_EINVAL, "loopback all-gather %lld: rank %d called again before every rank called "
+                     "(loopback ranks must be stepped in lockstep)", (long long)L.seq, r);
+    if (L.arrived > 0 && count != L.count[std::find(L.have.begin(), L.have.end(), 1) - L.have.begin()])
+        return cfail(GGS_EINVAL, "loopback all-gather %lld: rank %d sends %lld floats, another rank a different "
+                     "count", (long long)L.seq, r, (long long)count);
+    DevScope ds(L.dev);
+    GGS_HIPC(hipEventRecord(L.ev[r], stream));
+    L.have[r] = 1;
+    L.st[r] = stream;
+    L.send[r] = d_send;
+    L.recv[r] = d_recv;
+    L.count[r] = count;
+    if (++L.arrived < L.n) return GGS_OK;
+    const size_t bytes = sizeof(float) * (size_t)count;
+    for (int q = 0; q < L.n; ++q) {               // rank q's stream receives every shard
+        for (int p = 0; p < L.n; ++p) {
+            float* dst = L.recv[q] + (int64_t)p * count;
+            if (p != q) GGS_HIPC(hipStreamWaitEvent(L.st[q], L.ev[p], 0));
+            if (bytes && dst != L.send[p])
+                GGS_HIPC(hipMemcpyAsync(dst, L.send[p], bytes, hipMemcpyDeviceToDevice, L.st[q]));
+        }
+        GGS_HIPC(hipEventRecord(L.done[q], L.st[q]));
+    }
+    for (int q = 0; q < L.n; ++q)
+        for (int p = 0; p < L.n; ++p)
+            if (p != q) GGS_HIPC(hipStreamWaitEvent(L.st[q], L.done[p], 0));
+    std::fill(L.have.begin(), L.have.end(), 0);
+    L.arrived = 0;
+    ++L.seq;
+    return GGS_OK;
+}
+
+int loop_allgather_host(Comm* c, const float* send, float* recv, int64_t count) {
+    Loop& L = *c->loop;
+    std::unique_lock<std::mutex> lk(L.mu);
+    if (L.harrived == 0) {
+        L.hcount = count;
+        L.hbuf.assign((size_t)L.n * (size_t)std::max<int64_t>(count, 0), 0.0f);
+    } else if (count != L.hcount) {
+        return cfail(GGS_EINVAL, "loopback host all-gather: rank %d sends %lld floats, rank(s) before it %lld",
+                     c->rank, (long long)count, (long long)L.hcount);
+    }
+    if (count > 0) memcpy(L.hbuf.data() + (int64_t)c->rank * count, send, sizeof(float) * (size_t)count);
+    const int64_t gen = L.hgen;
+    if (++L.harrived == L.n) {
+        L.hres.swap(L.hbuf);
+        L.harrived = 0;
+        ++L.hgen;
+        L.cv.notify_all();
+    } else {
+        const char* t = getenv("GGS_LOOPBACK_TIMEOUT_S");
+        const double secs = t ? atof(t) : 60.0;
+        if (!L.cv.wait_for(lk, std::chrono::duration<double>(secs), [&] { return L.hgen != gen; })) {
+            --L.harrived;
+            return cfail(GGS_EHIP, "loopback host all-gather: rank %d waited %.0f s for the other %d rank(s) "
+                         "(each loopback rank needs its own host thread)", c->rank, secs, L.n - L.harrived - 1);
+        }
+    }
+    if (count > 0) memcpy(recv, L.hres.data(), sizeof(float) * (size_t)count * L.n);
+    return GGS_OK;
+}
+
 }  // namespace
 }  // namespace ggs
 
@@ -198,8 +305,15 @@ int ggs_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t*
 
 int ggs_comm_allgather(void* comm, void* stream, const float* d_send, float* d_recv, int64_t count,
                        int32_t overlap, int64_t* ticket) {
-    const Rccl& R = rccl();
     Comm* c = (Comm*)comm;
+    if (c && c->loop) {
+        if (count < 0 || (count > 0 && (!d_send || !d_recv)))
+            return cfail(GGS_EINVAL, "ggs_comm_allgather: count %lld with null buffers", (long long)count);
+        if (overlap) return cfail(GGS_EINVAL, "ggs_comm_allgather: a loopback communicator gathers in-stream only");
+        if (ticket) *ticket = -1;
+        return loop_allgather(c, (hipStream_t)stream, d_send, d_recv, count);
+    }
+    const Rccl& R = rccl();
     if (!c || !R.ok) return cfail(GGS_EINVAL, "ggs_comm_allgather: no communicator");
     if (count < 0 || (count > 0 && (!d_send || !d_recv)))
         return cfail(GGS_EINVAL, "ggs_comm_allgather: count %lld with null buffers", (long long)count);
@@ -255,11 +369,13 @@ int ggs_comm_size(void* comm, int32_t* nranks, int32_t* rank) {
 void ggs_comm_destroy(void* comm) {
     Comm* c = (Comm*)comm;
     if (!c) return;
-    const Rccl& R = rccl();
     {
         DevScope ds(c->dev);
         if (c->side) (void)hipStreamSynchronize(c->side);
-        if (c->nc && R.ok) (void)R.comm_destroy(c->nc);
+        if (c->nc) {
+            const Rccl& R = rccl();
+            if (R.ok) (void)R.comm_destroy(c->nc);
+        }
         for (int i = 0; i < kTickets; ++i)
             if (c->done[i]) (void)hipEventDestroy(c->done[i]);
         if (c->ready) (void)hipEventDestroy(c->ready);
@@ -298,11 +414,12 @@ int ggs_comm_init_local(int32_t n, const int32_t* devices, void** comms) {
 }
 
 int ggs_comm_allgather_host(void* comm, const float* send, float* recv, int64_t count) {
-    const Rccl& R = rccl();
     Comm* c = (Comm*)comm;
-    if (!c || !R.ok) return cfail(GGS_EINVAL, "ggs_comm_allgather_host: no communicator");
     if (count < 0 || (count > 0 && (!send || !recv)))
         return cfail(GGS_EINVAL, "ggs_comm_allgather_host: count %lld with null buffers", (long long)count);
+    if (c && c->loop) return loop_allgather_host(c, send, recv, count);
+    const Rccl& R = rccl();
+    if (!c || !R.ok) return cfail(GGS_EINVAL, "ggs_comm_allgather_host: no communicator");
     std::lock_guard<std::mutex> lk(c->mu);
     DevScope ds(c->dev);
     const int64_t cnt = std::max<int64_t>(count, 1);    // a zero-length call still synchronises the ranks
@@ -326,6 +443,37 @@ int ggs_comm_allgather_host(void* comm, const float* send, float* recv, int64_t 
 }
 
 int ggs_comm_barrier(void* comm) { return ggs_comm_allgather_host(comm, nullptr, nullptr, 0); }
+
+int ggs_comm_init_loopback(int32_t device, int32_t n, void** comms) {
+    if (n < 1 || !comms) return cfail(GGS_EINVAL, "ggs_comm_init_loopback: need n >= 1 and outputs");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return cfail(GGS_ENODEV, "ggs_comm_init_loopback: device %d not available (%d visible)", device, ndev);
+    DevScope ds(device);
+    auto L = std::make_shared<Loop>();
+    L->n = n;
+    L->dev = device;
+    L->have.assign(n, 0);
+    L->st.assign(n, nullptr);
+    L->send.assign(n, nullptr);
+    L->recv.assign(n, nullptr);
+    L->count.assign(n, 0);
+    L->ev.assign(n, nullptr);
+    L->done.assign(n, nullptr);
+    for (int i = 0; i < n; ++i) {
+        GGS_HIPC(hipEventCreateWithFlags(&L->ev[i], hipEventDisableTiming));
+        GGS_HIPC(hipEventCreateWithFlags(&L->done[i], hipEventDisableTiming));
+    }
+    for (int i = 0; i < n; ++i) {
+        Comm* c = new Comm;
+        c->dev = device;
+        c->nranks = n;
+        c->rank = i;
+        c->loop = L;
+        comms[i] = c;
+    }
+    return GGS_OK;
+}
 
 }  // extern "C"
 

@@ -847,7 +847,10 @@ hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fi
     // path, N <= VT) up to 1,024 splats: the shipped GA run (config.py: 512 splats)
     // on the generic path (two splats per thread, the child rows round-tripping
     // through HBM between the passes) bred in 21.6 us per generation.
-    const int vt = N <= 256 ? 256 : N <= 512 ? 512 : 1024;
+    // Past 1,024 splats (the generic path, several splats per thread) 256 threads,
+    // unless the launch is too small to fill the chip (< 64 workgroups): the same
+    // rule for the breed (+ stats workgroup) and the plain variation launch.
+    const int vt = N <= 256 ? 256 : N <= 512 ? 512 : (N <= 1024 || n_off < 64) ? 1024 : 256;
 #define GGS_VAR(VTT, BR, NB, BD)                                                                  \
     hipLaunchKernelGGL((ga_variation_kernel<VTT, BR>), dim3(NB), dim3(VTT), 0, st, pop, fits, P, N, prm, d, k0, \
                        k1, gen, off, n_off, recs, bnds, H, W, k_sigma, sl, sit, BD)
@@ -856,12 +859,10 @@ hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fi
         if (vt == 256) GGS_VAR(256, true, n_off + 1, *br);
         else if (vt == 512) GGS_VAR(512, true, n_off + 1, *br);
         else GGS_VAR(1024, true, n_off + 1, *br);
-    } else if ((n_off < 64 && N >= 1024) || (N > 512 && N <= 1024)) {
-        GGS_VAR(1024, false, n_off, BreedDev{});
-    } else if (N > 256 && N <= 512) {
-        GGS_VAR(512, false, n_off, BreedDev{});
     } else {
-        GGS_VAR(256, false, n_off, BreedDev{});
+        if (vt == 256) GGS_VAR(256, false, n_off, BreedDev{});
+        else if (vt == 512) GGS_VAR(512, false, n_off, BreedDev{});
+        else GGS_VAR(1024, false, n_off, BreedDev{});
     }
 #undef GGS_VAR
     return hipGetLastError();

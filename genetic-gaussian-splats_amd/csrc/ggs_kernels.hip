@@ -40,6 +40,12 @@
 #include "ggs_internal.h"
 #include "ggs_prep.h"
 
+// The raster's folded finalize (strip_done) relies on gfx9-family store/vmcnt
+// semantics and the wave64 layout; this file is written for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "ggs_kernels.hip targets gfx950 (MI355X) only"
+#endif
+
 namespace ggs {
 
 using namespace detmath;
@@ -170,6 +176,11 @@ __device__ __forceinline__ void strip_done(const FinFused& fin, const float* par
         old = __hip_atomic_fetch_add(fin.ctr + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (ufirst(old) != nslots - 1) return;
+    // acquire at agent scope in the one wave that reduces: pairs with the other
+    // waves' drained write-through stores + count, so the partial loads below
+    // cannot be satisfied from before the count (HIP memory model, not only the
+    // ISA's vmcnt ordering); one wave per candidate pays it
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const float v = finalize_wave<true>(partials, fin.wpartials, nslots, fin.mode, fin.hw, b);
     if (lane == 0) {
         fin.out[b] = v;
@@ -260,7 +271,11 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 // (round 3: raster -1.0 %, bit-identical).  (Round 4 measured the clamp's
 // removal with 8 bx = -1e30 on the column-clipped lanes: raster -0.3 %, but the
 // configs[4] SA trajectory changed, so some state's splats rely on it.)
+#if defined(GGS_NO_RATIO_CLAMP) && GGS_NO_RATIO_CLAMP   // probe build only: does a parity test see it?
+#define GGS_RATIO(qy8) GGS_EXP2(__builtin_fmaf((qy8), s.c128, abx.y))
+#else
 #define GGS_RATIO(qy8) GGS_EXP2(fminf(__builtin_fmaf((qy8), s.c128, abx.y), 100.0f))
+#endif
 // The first pair's exponent e = qy (Cc qy + bx) + px for both rows of the pair,
 // as (qy/8) (64 Cc (qy/8) + 8 bx) + px (make_rec: the same bits).  64 Cc broadcast
 // from the low half of the record's (C64, cx) SGPR pair, 8 bx from the high half

@@ -142,7 +142,9 @@ __device__ __forceinline__ float ld_partial(const float* __restrict__ p) {
 }
 template <bool COHERENT = false>
 __device__ __forceinline__ double wave_sum(const float* __restrict__ x, int n) {
-    const int lane = threadIdx.x & 63;
+    // lane from mbcnt, not threadIdx.x: the raster's folded finalize would
+    // otherwise keep threadIdx.x live (and spilled) across its epilogue
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     double a = 0.0;
     int i = lane;
     // loads in flight in blocks (32, then 8), then the same in-order adds: the

@@ -101,6 +101,7 @@ SIGNATURES = {
     "ggs_comm_destroy": (None, [C.c_void_p]),
     "ggs_ga_set_comm": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ggs_comm_init_local": (C.c_int, [C.c_int32, _i32p, C.POINTER(C.c_void_p)]),
+    "ggs_comm_init_loopback": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     "ggs_comm_allgather_host": (C.c_int, [C.c_void_p, _f32p, _f32p, C.c_int64]),
     "ggs_comm_barrier": (C.c_int, [C.c_void_p]),
 }

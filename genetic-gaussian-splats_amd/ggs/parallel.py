@@ -300,3 +300,22 @@ class RcclGather:
             self.close()
         except Exception:
             pass
+
+
+def loopback_group(device: int, n: int) -> list:
+    """n communicators on ONE device of this process acting as ranks 0..n-1 of one
+    job (``ggs_comm_init_loopback``; a test rig, no RCCL): the sharded code paths
+    (rank != 0, uneven and empty shards, the GA's fingerprint exchange) run on a
+    one-GPU box.  Device all-gathers must be issued in lockstep (every rank once
+    per gather); host all-gathers need one host thread per rank.  Each returned
+    object has RcclGather's interface."""
+    from . import _lib
+    arr = (C.c_void_p * int(n))()
+    _lib.check(_lib.lib.ggs_comm_init_loopback(int(device), int(n), arr), "ggs_comm_init_loopback")
+    out = []
+    for r in range(int(n)):
+        g = RcclGather.__new__(RcclGather)
+        g._lib, g._C, g.rank, g.world, g.handle = _lib, C, r, int(n), C.c_void_p(arr[r])
+        out.append(g)
+    return out
+

@@ -268,6 +268,15 @@ void ggs_comm_destroy(void* comm);
  * exchange): comms[i] is rank i on devices[i].  The host API uses this for its
  * own multi-device fan-out (ggs_fitness with n_devices > 1). */
 int ggs_comm_init_local(int32_t n, const int32_t* devices, void** comms);
+/* Loopback group (test rig, no RCCL): n communicators on ONE device of this
+ * process acting as ranks 0..n-1 of one job, so a one-GPU box runs the sharded
+ * paths (rank != 0, uneven and empty shards, ggs_ga_set_comm's fingerprint
+ * check).  Device all-gathers are matched by call order: every rank calls once
+ * per gather (lockstep; a second call before all ranks called fails), the last
+ * call enqueues the shard copies on every rank's stream.  Host all-gathers /
+ * barriers block until all n ranks (on their own host threads) arrived, at most
+ * GGS_LOOPBACK_TIMEOUT_S seconds (default 60), then fail. */
+int ggs_comm_init_loopback(int32_t device, int32_t n, void** comms);
 /* Host-pointer all-gather (synchronous): recv[r*count + i] = rank r's send[i].
  * Staged through the communicator's own device buffer and stream; for small
  * control values (timings, session fingerprints).  count = 0: a barrier. */

@@ -219,3 +219,120 @@ def test_configs3_sharded_over_eight_slots_equals_unsharded(hip, monkeypatch):
     picks = [spans[0][0], spans[0][1] - 1, spans[world - 1][0], spans[world - 1][1] - 1]
     ref = np.asarray(O.fitness_many([pop[i] for i in picks], tgt, H, W, 3.0, weight_mask=mask))
     assert np.max(np.abs(got[picks] - ref) / np.abs(ref)) <= 1e-5
+
+
+# ---- loopback ranks: the sharded paths at world > 1 on one GPU ----------------------
+def _loop_problem(H, N, P, seed):
+    from ggs import ga
+    rng = np.random.default_rng(seed)
+    tgt = rng.uniform(0, 1, (H, H, 3)).astype(np.float32)
+    mask = rng.uniform(0.4, 1.0, (H, H)).astype(np.float32)
+    init = ga.new_population(P, N, H, H, 3.0, 0.1, np.random.default_rng(seed + 1))
+    cfg = dict(tour_k=2, elite_k=8, cxpb=0.05, mutpb=0.05, min_scale_splats=3.0, max_scale_splats=0.1,
+               seed=seed, schedule="cosine",
+               mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0, "alpha": 25.0},
+               mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0, "alpha": 2.0})
+    return tgt, mask, init, cfg
+
+
+def _set_comm_all(sessions, comms):
+    """ggs_ga_set_comm on every rank at once (its fingerprint exchange is a host
+    all-gather: one host thread per loopback rank); returns each rank's error."""
+    import threading
+    errs = [None] * len(sessions)
+
+    def one(r):
+        try:
+            sessions[r].set_comm(comms[r])
+        except Exception as e:  # noqa: BLE001 — reported per rank
+            errs[r] = e
+    ts = [threading.Thread(target=one, args=(r,)) for r in range(len(sessions))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    return errs
+
+
+@pytest.mark.parametrize("H,N,P", [(512, 512, 32), (512, 256, 128)], ids=["shipped", "bench"])
+@pytest.mark.parametrize("n", [2, 5, 7, 8])
+def test_device_ga_loopback_ranks_equal_unsharded(hip, H, N, P, n):
+    """The device GA's rank != 0 path (ggs_capi.cpp ga step: every rank breeds all
+    P offspring with the same draws, rasterises its block [b0, b0+nb) of the
+    P - E evaluated ones, per = ceil((P - E) / n), then one in-place all-gather of
+    `per` scalars from offset rank*per) with n ranks on one GPU through a loopback
+    group.  Shipped shape (config.py: 512^2, 512 splats, pop 32, elite 8 -> 24
+    evaluated): n = 2 and 8 even shards, 5 uneven (5,5,5,5,4), 7 with an empty
+    last rank (4 x 6 + 0).  Bench shape (pop 128 -> 120): 7 and 8 uneven.  Every
+    rank's 20-generation trajectory (population, fitness, best, curves) equals
+    the unsharded session's bit for bit (algorithm.py:123-141)."""
+    from ggs.ga_device import DeviceGA
+    from ggs.parallel import loopback_group
+    tgt, mask, init, cfg = _loop_problem(H, N, P, seed=21)
+    G = 20
+    solo = DeviceGA(tgt, mask, init, **cfg)
+    for g in range(1, G + 1):
+        solo.step(g, G)
+    ref = solo.read()
+    solo.close()
+    comms = loopback_group(0, n)
+    ranks = [DeviceGA(tgt, mask, init, **cfg) for _ in range(n)]
+    try:
+        errs = _set_comm_all(ranks, comms)
+        assert errs == [None] * n, errs
+        for g in range(1, G + 1):
+            for d in ranks:                  # lockstep: every rank once per generation
+                d.step(g, G)
+        for r, d in enumerate(ranks):
+            st = d.read()
+            np.testing.assert_array_equal(st["population"], ref["population"], err_msg=f"rank {r}")
+            np.testing.assert_array_equal(st["fitness"], ref["fitness"], err_msg=f"rank {r}")
+            assert st["best_fit"] == ref["best_fit"] and st["curves"] == ref["curves"], r
+    finally:
+        for d in ranks:
+            d.close()
+        for c in comms:
+            c.close()
+
+
+def test_device_ga_loopback_fingerprint_mismatch_fails_loudly(hip):
+    """One rank with a different seed: every rank's ggs_ga_set_comm refuses
+    (the shards would mix populations), naming the differing rank."""
+    from ggs.ga_device import DeviceGA
+    from ggs.parallel import loopback_group
+    tgt, mask, init, cfg = _loop_problem(64, 16, 24, seed=3)
+    n = 3
+    comms = loopback_group(0, n)
+    ranks = [DeviceGA(tgt, mask, init, **dict(cfg, seed=cfg["seed"] + (r == 2))) for r in range(n)]
+    try:
+        errs = _set_comm_all(ranks, comms)
+        assert all(isinstance(e, ggs.GGSInputError) for e in errs), errs
+        assert all("differs" in str(e) for e in errs), errs
+    finally:
+        for d in ranks:
+            d.close()
+        for c in comms:
+            c.close()
+
+
+def test_loopback_gather_out_of_lockstep_fails_loudly(hip):
+    """A rank that issues its next device gather before every rank issued the
+    current one fails (no silent reorder); a host gather with a rank missing
+    times out with an error instead of hanging."""
+    from ggs.parallel import loopback_group
+    comms = loopback_group(0, 2)
+    st = hip.Stream()
+    buf = hip.DeviceArray((4,))
+    try:
+        comms[0].allgather(st.handle, buf.ptr, buf.ptr, 2)
+        with pytest.raises(ggs.GGSInputError, match="lockstep"):
+            comms[0].allgather(st.handle, buf.ptr, buf.ptr, 2)
+        comms[1].allgather(st.handle, buf.ptr + 8, buf.ptr, 2)
+        st.synchronize()
+        os.environ["GGS_LOOPBACK_TIMEOUT_S"] = "1"
+        with pytest.raises(ggs.GGSError, match="waited"):
+            comms[0].barrier()
+    finally:
+        os.environ.pop("GGS_LOOPBACK_TIMEOUT_S", None)
+        for c in comms:
+            c.close()

@@ -303,26 +303,48 @@ def test_headline_config_matches_reference_golden():
     plan.close()
 
 
-def test_fused_finalize_bit_stable_under_concurrent_uneven_load():
-    """The finalize folded into the raster (the last strip wave of each candidate
-    reduces the partials other waves, on any XCD, stored write-through; agent-scope
-    loads, no fence) under uneven concurrent load: four streams with their own
-    plans and workspaces, batches of 128 / 37 / 1 candidates at 512^2 and 24 at
-    1024^2, 30 launches each, enqueued interleaved with no sync; every launch's
-    fitness vector equals, bit for bit, the same batch evaluated alone — and the
-    per-candidate counters re-arm (a second round of launches agrees too)."""
+@pytest.mark.parametrize("fold", [False, True], ids=["finalize_launch", "folded_finalize"])
+def test_fused_finalize_bit_stable_under_concurrent_uneven_load(fold, monkeypatch):
+    """Fitness under uneven concurrent load: four or five streams with their own
+    plans and workspaces, batches of 128 / 37 / 1 candidates at 512^2, 24 at
+    1024^2 and 8 at 1024^2 with 640 splats (the saturation-checking instance),
+    30 launches each, enqueued interleaved with no sync; every launch's fitness
+    vector equals, bit for bit, the same batch evaluated alone.
+
+    folded_finalize runs the fitness API with the finalize folded into the raster
+    (GGS_FITNESS_FOLD=1, the device GA's raster_kernel<1, *, true>): the last
+    strip wave of each candidate reduces partials other waves, on any XCD, stored
+    write-through, after an agent-scope acquire; the second round of launches
+    checks that the per-candidate counters re-arm.  finalize_launch is the
+    separate finalize kernel the fitness API uses by default."""
     from ggs import hip
     rng = np.random.default_rng(77)
     jobs = []
-    for H, B, seed in ((512, 128, 1), (512, 37, 2), (512, 1, 3), (1024, 24, 4)):
-        pop = O.synthetic_population(B, 256 if H == 512 else 512, H, H, seed=seed)
+    monkeypatch.delenv("GGS_FITNESS_FOLD", raising=False)
+    for H, B, N, seed in ((512, 128, 256, 1), (512, 37, 256, 2), (512, 1, 256, 3), (1024, 24, 512, 4),
+                          (1024, 8, 640, 5)):
+        pop = O.synthetic_population(B, N, H, H, seed=seed)
         tgt = rng.uniform(0, 1, (H, H, 3)).astype(np.float32)
         mask = rng.uniform(0.4, 1.0, (H, H)).astype(np.float32)
         st = hip.Stream()
         g, t, m = (hip.DeviceArray.from_host(a) for a in (pop, tgt, mask))
         plan = ggs.TargetPlan(0, st.handle, t.ptr, m.ptr, ggs.GGS_FIT_WEIGHTED, 1.0, H, H)
-        jobs.append(dict(H=H, B=B, N=pop.shape[1], st=st, g=g, t=t, m=m, plan=plan,
+        jobs.append(dict(H=H, B=B, N=N, st=st, g=g, t=t, m=m, plan=plan,
                          alone=ggs.fitness(pop, tgt, H, H, 3.0, weight_mask=mask)))
+    if fold:
+        monkeypatch.setenv("GGS_FITNESS_FOLD", "1")
+    # the path under test really runs: no finalize launch when folded
+    ggs.profile_reset()
+    ggs.profile_enable(True)
+    j0, o0 = jobs[0], hip.DeviceArray((jobs[0]["B"],))
+    j0["plan"].fitness_device(j0["st"].handle, j0["g"].ptr, j0["B"], j0["N"], 9, 3.0, o0.ptr)
+    j0["st"].synchronize()
+    n_fin = ggs.profile_read("finalize")[1]
+    n_ras = ggs.profile_read("raster")[1]
+    ggs.profile_enable(False)
+    ggs.profile_reset()
+    assert n_ras == 1 and n_fin == (0 if fold else 1), (n_ras, n_fin)
+    np.testing.assert_array_equal(o0.to_host(), j0["alone"])
     for _ in range(2):
         outs = [[hip.DeviceArray((j["B"],)) for _ in range(30)] for j in jobs]
         for i in range(30):
