@@ -123,6 +123,45 @@ def _summary(config="512"):
         return None, None
 
 
+def _norm_kernel(k):
+    return (k or "").replace("void ", "").replace("ggs::", "").strip()
+
+
+def lib_sha256(path):
+    import hashlib
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
+def profile_match(config, kernel, lib_sha):
+    """Whether the newest committed profile of this launch shape describes THIS
+    binary: its stamp (tools/prof_summary.py + tools/collect_profile.sh) must name
+    exactly the raster instance this launch runs and the sha256 of the libggs.so
+    this process loaded.  Returns (ok, reason, source)."""
+    d, src = _summary(config)
+    if d is None:
+        return False, "no committed profile of this launch shape", None
+    st = d.get("stamp") or {}
+    prof_k = st.get("raster_kernel")
+    if not prof_k:
+        return False, f"{src} is not stamped with the profiled raster kernel and library", src
+    if _norm_kernel(prof_k) != _norm_kernel(kernel):
+        return False, f"{src} profiled {prof_k}; this launch runs {kernel}", src
+    if st.get("libggs_sha256") != lib_sha:
+        return False, (f"{src} profiled libggs.so sha256 {str(st.get('libggs_sha256'))[:16]}; this run loaded "
+                       f"{str(lib_sha)[:16]}"), src
+    return True, f"{src}: same raster instance, same libggs.so (git {str(st.get('git_head'))[:12]})", src
+
+
+def _raster_counters(d):
+    st = (d or {}).get("stamp") or {}
+    k = st.get("raster_kernel")
+    return d["counters"][k] if k else None
+
+
 def pmc_traffic(config="512"):
     """HBM bytes per raster launch from the newest committed rocprofv3 PMC
     summary of this same workload (tools/profile.sh -> profiles/rNN[_<config>]/
@@ -137,13 +176,13 @@ def pmc_traffic(config="512"):
 def pmc_valu_busy(config="512"):
     """Fraction of SIMD cycles the raster kernel's VALU was busy, from the same
     committed PMC summary: SQ_ACTIVE_INST_VALU (quad-cycles, summed over SIMDs)
-    x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); None when absent."""
+    x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) of the stamped raster kernel;
+    None when absent."""
     d, _ = _summary(config)
     try:
-        cs = d["counters"]
-        c = cs[next(k for k in cs if "raster_kernel<1" in k)]
+        c = _raster_counters(d)
         return round(c["SQ_ACTIVE_INST_VALU"] * 4 / (c["GRBM_GUI_ACTIVE"] / 8 * 1024), 4)
-    except (TypeError, KeyError, ZeroDivisionError, StopIteration):
+    except (TypeError, KeyError, ZeroDivisionError):
         return None
 
 
@@ -152,10 +191,25 @@ def pmc_trace_avg_us(config="512"):
     single-stream bench pass (tools/profile.sh runs bench.py --streams 1)."""
     d, _ = _summary(config)
     try:
-        return d.get("raster_profile_pass_avg_us") or \
-            next(v["avg_us"] for k, v in d["kernels"].items() if "raster_kernel<1" in k)
-    except (AttributeError, StopIteration, KeyError):
+        k = d["stamp"]["raster_kernel"]
+        return d.get("raster_profile_pass_avg_us") or d["kernels"][k]["avg_us"]
+    except (AttributeError, KeyError, TypeError):
         return None
+
+
+def rocprof_kernel_ms(config="512"):
+    """Per-kernel average durations (ms) of the committed rocprofv3 trace of this
+    launch shape: prep, raster, finalize (the trace's own clock, beside the
+    HIP-event figures, which include each event pair's overhead)."""
+    d, _ = _summary(config)
+    out = {}
+    for name, key in (("prep", "prep_kernel<true>"), ("raster", None), ("finalize", "finalize_kernel")):
+        try:
+            k = d["stamp"]["raster_kernel"] if key is None else next(x for x in d["kernels"] if key in x)
+            out[name] = round(d["kernels"][k]["avg_us"] / 1e3, 5)
+        except (AttributeError, KeyError, TypeError, StopIteration):
+            out[name] = None
+    return out
 
 
 def profile_config(config, pop_arg, per_gpu):
@@ -763,17 +817,23 @@ def run(args, world, rank, local_rank, distributed):
         # rNN_<config>): configs[3] split over 8 ranks launches configs[2]'s 512 per GPU;
         # a --pop exploration has none
         prof_cfg = profile_config(args.config, args.pop, POP)
-        profiled = prof_cfg is not None
+        kernel = "raster_kernel<1, false, false>" if N_SPLATS <= 512 else "raster_kernel<1, true, false>"
+        # PMC figures only from a profile of THIS binary and THIS raster instance
+        match, match_why, match_src = profile_match(prof_cfg, kernel, lib_sha256(ggs.LIB_PATH)) \
+            if prof_cfg is not None else (False, "no committed profile of this launch shape (--pop)", None)
+        profiled = match
         traffic, traffic_src = pmc_traffic(prof_cfg) if profiled else (None, None)
         valu_tflops = FLOP_PER_PAIR * pairs_per_cand * POP / (raster_ms * 1e-3) / 1e12
         busy = pmc_valu_busy(prof_cfg) if profiled else None
-        _, busy_src = _summary(prof_cfg) if profiled else (None, None)
+        busy_src = match_src if profiled else None
+        rp = rocprof_kernel_ms(prof_cfg) if profiled else {}
+        ev_sum = sum(v[0] / max(v[1], 1) for v in kern.values())
         # The raster is bound by the VALU: `bound` names
         # that roof.  achieved / peak / frac are the HBM figures the contract defines
         # (algorithmic bytes per launch / HIP-event launch time vs 8 TB/s, frac_roof);
         # the VALU's executed-work fraction is binding_frac (PMC busy).
-        roof = {"bound": "valu", "kernel": "raster_kernel<1, false, false>" if N_SPLATS <= 512 else
-                "raster_kernel<1, true, false>",
+        roof = {"bound": "valu", "kernel": kernel,
+                "profile_match": {"ok": match, "why": match_why, "libggs_sha256": lib_sha256(ggs.LIB_PATH)},
                 "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "frac_roof": "hbm",
                 "traffic": None if traffic is None else round(traffic),
@@ -845,6 +905,13 @@ def run(args, world, rank, local_rank, distributed):
             "host_enqueue_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "host_api_renders_per_s": host_api,
             "kernels_ms_per_launch": {k: round(v[0] / max(v[1], 1), 5) for k, v in kern.items()},
+            "kernels_ms_rocprof": (rp or None) if kern else None,
+            "kernel_timing_note": (None if not kern else
+                                   f"HIP events bracket each launch on its stream (one event pair per kernel): "
+                                   f"prep + raster + finalize sum to {ev_sum:.4f} ms against a "
+                                   f"{extras.get('ms_per_step_one_stream', float('nan')):.4f}-ms one-stream step, "
+                                   f"so each event figure carries the pair's overhead and the launch gap; "
+                                   f"kernels_ms_rocprof is the committed trace of the same binary"),
             "hip_runtime": _mapped("libamdhip64"),
             "torch_loaded": "torch" in sys.modules,
             "cpu_baseline": cpu,

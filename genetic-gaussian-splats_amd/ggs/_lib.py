@@ -173,7 +173,12 @@ def _load() -> C.CDLL:
             f"`make -C {os.path.join(_PKG_ROOT, 'csrc')}` (or __graft_entry__.build()). "
             "There is no CPU fallback.")
     lib = C.CDLL(LIB_PATH)
+    # an older build loaded for an A/B timing (GGS_LIB=libggs_<rev>.so) may lack
+    # entry points added since; the in-tree product library must have all of them
+    alt = "GGS_LIB" in os.environ and os.path.basename(LIB_PATH) != "libggs.so"
     for name, (res, args) in SIGNATURES.items():
+        if alt and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -224,6 +224,7 @@ def install_fake_gpu(mesh, rank, world, log, slow_rank=None, corrupt=False, stal
     ggs = types.ModuleType("ggs")
     ggs.hip = hip
     ggs.GGS_FIT_WEIGHTED = 1
+    ggs.LIB_PATH = os.path.join(PKG, "libggs.so")    # the built library (bench hashes it)
     ggs.ensure_init = lambda: max(world, 1)
     ggs.select_devices = lambda ids: log.__setitem__("selected", list(ids))
     ggs.TargetPlan = TargetPlan

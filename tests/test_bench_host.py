@@ -43,6 +43,50 @@ def test_pmc_figures_come_from_this_workloads_profile():
     assert 0.3 < busy < 1.0
 
 
+def _built_lib():
+    return os.path.join(REPO, "genetic-gaussian-splats_amd", "libggs.so")
+
+
+def test_committed_profiles_are_of_the_shipped_binary():
+    """The newest committed profile of each bench config (what bench.py quotes
+    traffic, VALU busy and rocprof times from) was taken on exactly the library
+    this tree builds (sha256 of libggs.so; the build is reproducible) and names
+    exactly the raster instance that config launches — so a kernel change without
+    a re-profile fails here, not silently in the bench line (round 4: the
+    profiles predated the last raster commit)."""
+    import json
+    sha = bench.lib_sha256(_built_lib())
+    assert sha
+    for cfg, kernel in (("512", "raster_kernel<1, false, false>"), ("1024", "raster_kernel<1, true, false>"),
+                        ("1024x8", "raster_kernel<1, true, false>")):
+        d, src = bench._summary(cfg)
+        assert d is not None, cfg
+        st = d.get("stamp") or {}
+        assert bench._norm_kernel(st.get("raster_kernel")) == kernel, (src, st.get("raster_kernel"))
+        assert st.get("libggs_sha256") == sha, (src, "profiled a different libggs.so: re-profile")
+        assert st.get("git_head") and st.get("git_tree_dirty") is False, src
+        ok, why, _ = bench.profile_match(cfg, kernel, sha)
+        assert ok, why
+        assert bench.rocprof_kernel_ms(cfg)["raster"] > 0
+        json.dumps(d)
+
+
+def test_profile_mismatch_drops_the_pmc_figures(monkeypatch):
+    """A summary of another build or another raster instance is refused with a
+    reason (bench.py then reports traffic / binding_frac as null)."""
+    d = {"stamp": {"raster_kernel": "void ggs::raster_kernel<1, false, false>", "libggs_sha256": "ab" * 32},
+         "counters": {}, "kernels": {}}
+    monkeypatch.setattr(bench, "_summary", lambda config="512": (d, "profiles/rXX/summary.json"))
+    ok, why, _ = bench.profile_match("512", "raster_kernel<1, false, false>", "cd" * 32)
+    assert not ok and "sha256" in why
+    ok, why, _ = bench.profile_match("512", "raster_kernel<1, true, false>", "ab" * 32)
+    assert not ok and "raster_kernel<1, false, false>" in why
+    ok, _, _ = bench.profile_match("512", "raster_kernel<1, false, false>", "ab" * 32)
+    assert ok
+    d["stamp"] = {}
+    assert not bench.profile_match("512", "raster_kernel<1, false, false>", "ab" * 32)[0]
+
+
 # ---- --gpus N: the rank spawn (no GPU: a stand-in script records what it got) ----
 _FAKE_RANK = r'''
 import json, os, sys
@@ -153,6 +197,9 @@ def test_bench_line_names_its_roofs_and_value_semantics(tmp_path):
     assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-4
     busy = bench.pmc_valu_busy()
     assert valu["frac"] == busy == roof["binding_frac"] and 0 < busy < 1
+    assert roof["profile_match"]["ok"], roof["profile_match"]
+    assert roof["traffic"] and roof["rocprof_trace_avg_ms"] > 0
+    assert line["kernels_ms_rocprof"]["raster"] > 0 and "one-stream step" in line["kernel_timing_note"]
     assert valu["frac_source"].startswith("profiles/r") and "SQ_ACTIVE_INST_VALU" in valu["frac_definition"]
     assert "frac" not in valu["reference_equivalent"] and "ratio_to_peak" in valu["reference_equivalent"]
     sem = line["value_semantics"]

@@ -25,5 +25,20 @@ with open(sys.argv[2], "w", newline="") as f:
                     int(r["End_Timestamp"]) - int(r["Start_Timestamp"])])
 PY
 done
-cp "$SRC/summary.json" "$SRC/commands.txt" "$DST/"
+cp "$SRC/commands.txt" "$DST/"
+# stamp the git revision: only when this tree's libggs.so is the profiled build
+python3 - "$SRC/summary.json" "$DST/summary.json" <<'PY'
+import hashlib, json, subprocess, sys
+d = json.load(open(sys.argv[1]))
+st = d.setdefault("stamp", {})
+lib = st.get("libggs") or "genetic-gaussian-splats_amd/libggs.so"
+mine = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+if st.get("libggs_sha256") != mine:
+    sys.exit(f"collect_profile: {lib} here ({mine[:16]}) is not the profiled build "
+             f"({str(st.get('libggs_sha256'))[:16]}): rebuild from the profiled revision or re-profile")
+git = lambda *a: subprocess.run(["git", *a], capture_output=True, text=True).stdout.strip()
+st["git_head"] = git("rev-parse", "HEAD")
+st["git_tree_dirty"] = bool(git("status", "--porcelain", "--", "genetic-gaussian-splats_amd/csrc", "include"))
+json.dump(d, open(sys.argv[2], "w"), indent=1)
+PY
 echo "copied $SRC -> $DST"

@@ -2,10 +2,20 @@
 per-launch counter means; HBM traffic per launch with the gfx950 corrections of
 MI355X_MICROARCH.md §HBM (FETCH_SIZE reports 1/2 of the bytes of wide streaming
 reads -> x2; WRITE_SIZE exact for 16-B streaming stores; both in KiB)."""
-import collections, csv, glob, json, os, sys
+import collections, csv, glob, hashlib, json, os, sys
 
 root = sys.argv[1]
 out = {"kernels": {}, "counters": {}}
+# What was profiled: the library file (sha256; bench.py compares it with the library
+# it runs and drops the PMC figures on a mismatch), the command, and below the raster
+# kernel's full symbol.  tools/collect_profile.sh adds the git revision (the box has
+# no .git) after checking that the tree's own build has this hash.
+_repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_lib = os.environ.get("GGS_LIB") or os.path.join(_repo, "genetic-gaussian-splats_amd", "libggs.so")
+out["stamp"] = {"libggs": os.path.relpath(_lib, _repo),
+                "libggs_sha256": hashlib.sha256(open(_lib, "rb").read()).hexdigest()
+                if os.path.exists(_lib) else None,
+                "command": os.environ.get("BENCH")}
 stats = os.path.join(root, "trace", "run_kernel_stats.csv")
 if os.path.exists(stats):
     for r in csv.DictReader(open(stats)):
@@ -32,6 +42,9 @@ for f in glob.glob(os.path.join(root, "pmc_*", "run_counter_collection.csv")):
         agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in agg.items():
     out["counters"][k] = {c: sum(v) / len(v) for c, v in cs.items()}
+rasters = sorted({k for k in list(out["counters"]) + list(out["kernels"]) if "raster_kernel" in k})
+out["stamp"]["raster_kernels"] = rasters
+out["stamp"]["raster_kernel"] = rasters[0] if len(rasters) == 1 else None
 r = next((k for k in out["counters"] if "raster_kernel" in k), None)
 if r:
     c = out["counters"][r]
