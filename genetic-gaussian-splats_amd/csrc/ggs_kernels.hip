@@ -33,6 +33,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <utility>
 #include <vector>
 
@@ -308,7 +309,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
-              const float* __restrict__ clean, const int* __restrict__ live, int CH, FinFused fin) {
+              const float* __restrict__ clean, const int* __restrict__ live, int CH, FinFused fin, int simds) {
     __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
 
     const int lane = threadIdx.x & 63;
@@ -330,6 +331,17 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     // Large launches run in candidate chunks of CH (all groups of one chunk, then
     // the next), so a chunk's records stay cached while its groups run
     int idx = blockIdx.x, b0 = 0, Bc = B;
+    // A launch of at most 3 strip-waves per SIMD runs in one round: every wave is
+    // resident from the start and the three sharing a SIMD (blocks r, r + S,
+    // r + 2S, S = SIMDs) split its VALU, so the SIMD ends with the SUM of their
+    // work (docs/EXPERIMENTS.md §14).  The middle third runs reversed: the
+    // heaviest (central) strips then share a SIMD with the lightest of the
+    // middle third instead of its heaviest (a boustrophedon over the expected
+    // cost order; the bits do not depend on the order)
+    if (simds > 0) {
+        const int n = B * nTiles * SPB;
+        if (n <= 3 * simds && idx >= simds && idx < min(2 * simds, n)) idx = simds + (min(2 * simds, n) - 1 - idx);
+    }
     if (B > CH) {
         const int per = CH * nTiles * SPB;
         const int c = idx / per;
@@ -737,10 +749,13 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             for (int g = 0; g < RG; ++g) {
                 const int row = ty0 + 4 * g + ph;
                 if (row < H) {
+                    // streaming (non-temporal) stores: the image is never re-read by this
+                    // launch, and write-allocating 384 MiB per 512^2/128 launch in L2
+                    // evicts the records and cull bounds every strip-wave re-reads
                     float* o = img + (((int64_t)b * H + row) * W + col) * 3;
-                    o[0] = fminf(fmaxf(__builtin_fmaf(T[g], bg_r, R[g]), 0.0f), 1.0f);
-                    o[1] = fminf(fmaxf(__builtin_fmaf(T[g], bg_g, G[g]), 0.0f), 1.0f);
-                    o[2] = fminf(fmaxf(__builtin_fmaf(T[g], bg_b, Bl[g]), 0.0f), 1.0f);
+                    __builtin_nontemporal_store(fminf(fmaxf(__builtin_fmaf(T[g], bg_r, R[g]), 0.0f), 1.0f), o + 0);
+                    __builtin_nontemporal_store(fminf(fmaxf(__builtin_fmaf(T[g], bg_g, G[g]), 0.0f), 1.0f), o + 1);
+                    __builtin_nontemporal_store(fminf(fmaxf(__builtin_fmaf(T[g], bg_b, Bl[g]), 0.0f), 1.0f), o + 2);
                 }
             }
         }
@@ -1017,6 +1032,21 @@ int raster_chunk(int N) {
     return ch < 8 ? 8 : (int)ch;
 }
 
+// SIMDs of the current device (CUs x 4), for the single-round block order; 0 if
+// unknown (no reordering)
+int raster_simds() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    static std::atomic<int> cached[64];          // zero-initialised (static storage)
+    if (dev >= 0 && dev < 64) {
+        const int c = cached[dev].load(std::memory_order_relaxed);
+        if (c) return c;
+    }
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (dev >= 0 && dev < 64) cached[dev].store(4 * cus, std::memory_order_relaxed);
+    return 4 * cus;
+}
+
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty, const float* clean,
@@ -1026,11 +1056,12 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const i
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
     const int CH = raster_chunk(N);
     const FinFused ff = (mode != 0 && fin) ? *fin : FinFused{};
+    const int simds = raster_simds();
     // FUSED is a template parameter, so the instances without the fold carry none
     // of its code (a runtime test left the SA raster 1 % slower than round 3's)
 #define GGS_RASTER(M, S, F)                                                                    \
     hipLaunchKernelGGL((raster_kernel<M, S, F>), grid, block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
-                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH, ff)
+                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH, ff, simds)
     // the saturation check only where strip lists can grow long (N > SAT_MIN_SPLATS);
     // at the bench's 256 splats the kernel without it is the faster code (+1.6 %)
     const bool sat = N > SAT_MIN_SPLATS;

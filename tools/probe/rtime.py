@@ -2,7 +2,7 @@
 stream) and one-stream step ms (prep + raster + finalize, dependent batches) at a
 bench config, each build in its own process, builds alternated for --rounds.
 
-    python tools/probe/rtime.py [--config 512|1024|1024x8|sa16|sa2] [--rounds 3] lib1.so lib2.so ...
+    python tools/probe/rtime.py [--config 512|1024|1024x8|sa16|sa2|sa1|ga24] [--rounds 3] lib1.so lib2.so ...
 
 Prints one line per (round, lib) and a median summary; --check compares every
 build's fitness vector with the first's (bit-identical or the max relative diff).
@@ -18,7 +18,8 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CFG = {"512": (512, 256, 128), "1024": (1024, 1024, 512), "1024x8": (1024, 1024, 4096), "sa16": (2048, 4096, 16),
-       "sa2": (2048, 4096, 2), "ga24": (512, 512, 24)}   # ga24: the shipped GA run's launch (config.py)
+       "sa2": (2048, 4096, 2), "sa1": (2048, 4096, 1),    # sa1: a lone SA neighbour (start of a run)
+       "ga24": (512, 512, 24)}   # ga24: the shipped GA run's launch (config.py)
 
 
 def worker(cfg, steps, out_npy):
@@ -71,7 +72,7 @@ def main():
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    steps = a.steps or {"512": 300, "1024": 20, "1024x8": 4, "sa16": 60, "sa2": 200, "ga24": 600}[a.config]
+    steps = a.steps or {"512": 300, "1024": 20, "1024x8": 4, "sa16": 60, "sa2": 200, "sa1": 300, "ga24": 600}[a.config]
     if a.worker:
         worker(a.config, steps, a.out)
         return

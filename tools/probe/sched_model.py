@@ -116,3 +116,31 @@ def split_model(pop, size, extra=300.0):
     cf = strip_costs(pop[:, N // 2:], size) + extra
     cb = strip_costs(pop[:, :N // 2], size) + extra
     return cf, cb
+
+
+def simulate_fixed(work, n_simd=1024):
+    """Single-round launch placed as the hardware does it (EXP §14: blocks r,
+    r + 1,024, r + 2,048 share SIMD r): the makespan under processor sharing."""
+    n = len(work)
+    per = -(-n // n_simd)
+    loads = np.zeros((n_simd, per))
+    for i, w in enumerate(work):
+        loads[i % n_simd, i // n_simd] = w
+    t_end = np.zeros(n_simd)
+    for s in range(n_simd):
+        rem = sorted(x for x in loads[s] if x > 0)
+        t, prev = 0.0, 0.0
+        k = len(rem)
+        for x in rem:                      # processor sharing: shortest finishes first
+            rate = TPUT[k] / k
+            t += (x - prev) / rate
+            prev = x
+            k -= 1
+        t_end[s] = t
+    return t_end.max()
+
+
+def group_order_blocks(cost, order):
+    """Block-order work of a launch whose strip groups run in `order` (candidates rotating)."""
+    B, G = cost.shape
+    return np.array([cost[(i + gi) % B, order[gi]] for gi in range(G) for i in range(B)])

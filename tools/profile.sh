@@ -14,6 +14,7 @@ export TMPDIR=/tmp
 # the profiled command (default: the bench workload); another config:
 #   BENCH="python3 bench.py --config 1024 --steps 10 --warmup 2 --no-cpu-baseline" PROF_STEPS=10 tools/profile.sh r01_1024
 BENCH=${BENCH:-"python3 bench.py --streams 1 --steps 30 --warmup 5 --min-time 0.05 --ramp-ms 100 --no-cpu-baseline --extras 0"}
+export BENCH                     # tools/prof_summary.py stamps the command
 run() { local name=$1; shift; echo "== $name: $*" | tee -a "$OUT/commands.txt"; timeout -k 10 300 "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }; }
 run trace rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- $BENCH
 run pmc_fetch rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- $BENCH
