@@ -331,16 +331,18 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     // Large launches run in candidate chunks of CH (all groups of one chunk, then
     // the next), so a chunk's records stay cached while its groups run
     int idx = blockIdx.x, b0 = 0, Bc = B;
-    // A launch of at most 3 strip-waves per SIMD runs in one round: every wave is
+    // A launch of 2-3 strip-waves per SIMD runs in one round: every wave is
     // resident from the start and the three sharing a SIMD (blocks r, r + S,
     // r + 2S, S = SIMDs) split its VALU, so the SIMD ends with the SUM of their
     // work (docs/EXPERIMENTS.md §14).  The middle third runs reversed: the
     // heaviest (central) strips then share a SIMD with the lightest of the
     // middle third instead of its heaviest (a boustrophedon over the expected
-    // cost order; the bits do not depend on the order)
+    // cost order; the bits do not depend on the order).  Shipped GA launch
+    // (24 x 128 strips) raster -1.45 %; with two waves per SIMD (a lone 2048^2
+    // SA neighbour) the pairing measured +1.05 %, so only above 2S (EXP §15)
     if (simds > 0) {
         const int n = B * nTiles * SPB;
-        if (n <= 3 * simds && idx >= simds && idx < min(2 * simds, n)) idx = simds + (min(2 * simds, n) - 1 - idx);
+        if (n > 2 * simds && n <= 3 * simds && idx >= simds && idx < 2 * simds) idx = 3 * simds - 1 - idx;
     }
     if (B > CH) {
         const int per = CH * nTiles * SPB;

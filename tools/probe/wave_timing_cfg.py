@@ -31,6 +31,25 @@ buf = np.zeros((n_waves, 8), np.uint64)
 fn = ggs.lib.ggs_debug_timing_read
 fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_size_t]
 assert fn(buf.ctypes.data, buf.nbytes) == 0, "not a GGS_TIMING build?"
+def slot_gaps(buf, s_us, e_us):
+    """Idle time between consecutive waves of one wave slot: HW_ID's wave / SIMD /
+    CU / SH / SE fields (bits 0-15) + XCC_ID name the slot; the gap is the next
+    wave's start minus this wave's end.  frac = the gaps over (slots x span)."""
+    key = ((buf[:, 5] & np.uint64(0xFFFF)) | ((buf[:, 5] >> np.uint64(32) & np.uint64(0xF)) << np.uint64(16))).astype(np.int64)
+    gaps, slots = [], 0
+    for k in np.unique(key):
+        i = np.where(key == k)[0]
+        i = i[np.argsort(s_us[i])]
+        slots += 1
+        if len(i) > 1:
+            gaps.extend((s_us[i[1:]] - e_us[i[:-1]]).tolist())
+    g = np.asarray(gaps) if gaps else np.zeros(1)
+    span = float(e_us.max())
+    return {"slots": slots, "waves_per_slot": round(len(s_us) / max(slots, 1), 2),
+            "gap_us": {q: round(float(np.percentile(g, p)), 3) for q, p in (("p10", 10), ("p50", 50), ("p90", 90))},
+            "gap_us_mean": round(float(g.mean()), 3), "gaps_frac_of_slot_time": round(float(g.sum()) / (slots * span), 4)}
+
+
 rt0, rt1 = buf[:, 0].astype(np.int64), buf[:, 1].astype(np.int64)
 t0 = rt0.min()
 s_us, e_us = (rt0 - t0) / 100.0, (rt1 - t0) / 100.0
@@ -58,6 +77,7 @@ res = {"H": H, "splats": a.splats, "batch": a.batch, "waves": n_waves, "span_us"
        "xcd_work_ms": [round(float(dur[xcc == x].sum()) / 1e3, 2) for x in range(8)],
        "xcd_end_us": [round(float(e_us[xcc == x].max()), 1) for x in range(8)],
        "xcd_live_mid_mean": [round(float(per_xcd_live[mid, x].mean()), 1) for x in range(8)],
+       "slot_gaps": slot_gaps(buf, s_us, e_us),
        "xcd_live_mid_max": [int(per_xcd_live[mid, x].max()) for x in range(8)],
        "xcd_full_frac_mid": float((per_xcd_live[mid] >= 384).any(axis=1).mean())}
 print(json.dumps(res))
