@@ -8,6 +8,7 @@ set -eu
 cd "$(dirname "$0")/.."
 TAG=${1:-r03}
 SRC=gpurun_out/prof_$TAG
+[ -d "$SRC" ] || SRC=gpurun_out/pack_$TAG      # packed on the box (tools/pack_profile.sh)
 DST=profiles/$TAG
 mkdir -p "$DST"
 cp "$SRC/trace/run_kernel_stats.csv" "$DST/kernel_stats.csv"

@@ -51,6 +51,7 @@ if [ "$PART" = A ]; then
 elif [ "$PART" = B ]; then
   bash tools/ga_default.sh ${TAG}_ga_default > gpurun_out/${TAG}_ga_default.log 2>&1; ok $? ga_default
   tail -12 gpurun_out/${TAG}_ga_default.log | cut -c1-300
+  bash tools/pack_profile.sh ${TAG}_ga_default
   for run in start late; do
     args=""; [ $run = late ] && args="--warm 2000 --temp0 1e-6"
     timeout -k 10 400 python3 tools/bench_sa.py --only device_loop_full --repeat 3 $args > gpurun_out/${TAG}_sa_$run.json 2>&1
@@ -60,8 +61,10 @@ elif [ "$PART" = B ]; then
   BENCH="python3 tools/bench_sa.py --only device_loop_full --dev-iters 100 --repeat 1" \
       bash tools/profile.sh ${TAG}_sa > gpurun_out/${TAG}_sa_profile.log 2>&1; ok $? profile_sa
   show gpurun_out/prof_${TAG}_sa/summary.json
+  bash tools/pack_profile.sh ${TAG}_sa
   bash tools/profile_sa_late.sh ${TAG}_sa_late > gpurun_out/${TAG}_sa_late_profile.log 2>&1; ok $? profile_sa_late
   show gpurun_out/prof_${TAG}_sa_late/summary.json
+  bash tools/pack_profile.sh ${TAG}_sa_late
 else
   echo "part must be A or B"; exit 2
 fi
