@@ -488,7 +488,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             // The empty asm keeps the compiler from if-converting it back into an
             // unconditional compare + select).  Dead lanes: px = -inf (f = 0; the
             // ratio's clamp keeps their walk at 0, see GGS_RATIO).
-            if (max(x0 - sx0, sx0 + 15 - x1) > 0) {
+            if (__builtin_expect(max(x0 - sx0, sx0 + 15 - x1) > 0, 0)) {
                 const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
                 px = inx ? px : -__builtin_inff();
                 asm volatile("" : "+v"(px));
@@ -625,7 +625,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     }
 #define GGS_MID3(k, k1, k2, k3)                                                         \
     u##k:                                                                               \
-        if (kB > (k3)) {                                                                \
+        if (__builtin_expect(kB > (k3), 1)) {                                           \
             GGS_BLEND_REC(k1) GGS_BLEND_REC(k2)                                         \
             if ((k3) == NPK - 1) {                                                      \
                 GGS_LASTF(k3)                                                           \
@@ -646,11 +646,14 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         }                                                                               \
         GGS_LASTB(k1)                                                                   \
         goto done;
-            GGS_MID3(0, 1, 2, 3) GGS_MID3(1, 2, 3, 4) GGS_MID3(2, 3, 4, 5) GGS_MID3(3, 4, 5, 6)
-            GGS_MID3(4, 5, 6, 7) GGS_MID3(5, 6, 7, 8) GGS_MID3(6, 7, 8, 9) GGS_MID3(7, 8, 9, 10)
-            GGS_MID3(8, 9, 10, 11) GGS_MID3(9, 10, 11, 12) GGS_MID3(10, 11, 12, 13)
-            GGS_MID3(11, 12, 13, 14) GGS_MID3(12, 13, 14, 15)
-#undef GGS_MID3
+            // laid out as three chains (u0 u3 u6 u9 u12 u15, u1 u4 ... u13, u2 u5 ...
+            // u14), so a walk continuing past its step falls through into the next
+            // step instead of taking a branch every three pairs
+            GGS_MID3(0, 1, 2, 3) GGS_MID3(3, 4, 5, 6) GGS_MID3(6, 7, 8, 9) GGS_MID3(9, 10, 11, 12)
+            GGS_MID3(12, 13, 14, 15)
+        u15:
+            goto done;
+            GGS_MID3(1, 2, 3, 4) GGS_MID3(4, 5, 6, 7) GGS_MID3(7, 8, 9, 10) GGS_MID3(10, 11, 12, 13)
         u13:                          // pairs 14 and 15 are the last ones there are
             if (kB == NPK) {
                 GGS_BLEND_REC(14)
@@ -664,6 +667,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             }
             GGS_LASTB(14)
             goto done;
+            GGS_MID3(2, 3, 4, 5) GGS_MID3(5, 6, 7, 8) GGS_MID3(8, 9, 10, 11) GGS_MID3(11, 12, 13, 14)
         u14:
             if (kB == NPK) {
                 GGS_LASTF(15)
@@ -671,10 +675,9 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             }
             GGS_LASTB(15)
             goto done;
+#undef GGS_MID3
 #undef GGS_LASTB
 #undef GGS_LASTF
-        u15:
-            goto done;
             // exact walk (guard tripped): the exponent per pair as before
 #define GGS_XMID(kp, k) x##kp: if (kB == k) goto xlast; if (k < NPK) GGS_PK(k, false);
             GGS_XMID(0, 1) GGS_XMID(1, 2) GGS_XMID(2, 3) GGS_XMID(3, 4) GGS_XMID(4, 5)
@@ -706,11 +709,11 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         SplatRec ra = load_at(0);
         int jr = 63;                  // last j before the next 64 offsets are needed
         for (int j = 0;;) {
-            if (j == jr) { jr += 64; offv = list[min(j + 1 + lane, cnt - 1)]; }
+            if (__builtin_expect(j == jr, 0)) { jr += 64; offv = list[min(j + 1 + lane, cnt - 1)]; }
             const SplatRec rb = load_at(j + 1);
             visit(ra);
             if (++j >= cnt) break;
-            if (j == jr) { jr += 64; offv = list[min(j + 1 + lane, cnt - 1)]; }
+            if (__builtin_expect(j == jr, 0)) { jr += 64; offv = list[min(j + 1 + lane, cnt - 1)]; }
             ra = load_at(j + 1);
             visit(rb);
             if (++j >= cnt) break;
