@@ -143,6 +143,17 @@ int ensure_tile_order(Workspace* w, int H, int W, hipStream_t st) {
     if ((rc = ensure(w->order, sizeof(int) * (size_t)n, st))) return rc;
     std::vector<int> h(n);
     raster_tile_order(H, W, h.data());
+#ifdef GGS_PROBE_BUILD
+    // probe: a dispatch order from a file of n int32 group indices (order experiments)
+    if (const char* f = getenv("GGS_PROBE_ORDER")) {
+        FILE* fp = fopen(f, "rb");
+        if (!fp || fread(h.data(), sizeof(int), n, fp) != (size_t)n) {
+            if (fp) fclose(fp);
+            return fail(GGS_EINVAL, "GGS_PROBE_ORDER: cannot read the order");
+        }
+        fclose(fp);
+    }
+#endif
     GGS_HIP(hipStreamSynchronize(st));
     GGS_HIP(hipMemcpy(w->order.p, h.data(), sizeof(int) * n, hipMemcpyHostToDevice));
     w->order_H = H;

@@ -113,6 +113,15 @@ constexpr int OCC = 3;            // waves per SIMD the register budget is sized
 constexpr int XCD_SHIFT = 3;
 constexpr int CULL_PRIO = 2;      // s_setprio while culling (1 and 3 measured the same)
 
+// Depth-split experiment (probe build only, docs/EXPERIMENTS.md §15): the fitness
+// instances without the saturation check (N <= SAT_MIN_SPLATS) run two waves per
+// strip; wave 0 culls the front half of the splat indices, wave 1 the back half,
+// each blends half of the joint list, and wave 0 composes the halves with the
+// associative "over" (C = C_f + T_f C_b, T = T_f T_b) through LDS.
+#ifndef GGS_DEPTH_SPLIT
+#define GGS_DEPTH_SPLIT 0
+#endif
+
 #ifndef GGS_NOPLAN
 #define GGS_NOPLAN 0      // probe build only (docs/EXPERIMENTS.md §4 traffic split): the epilogue reads no plan
 #endif
@@ -303,14 +312,15 @@ __device__ __forceinline__ f2_t fma2(f2_t a, f2_t b, f2_t c) { return __builtin_
 // preserving LDS list), blends that list front-to-back, and writes its own
 // partial sum.  TILE_H = 128: 128 accumulator VGPRs (+~35) -> 3 waves per SIMD.
 template <int MODE, bool SAT, bool FUSED>
-__global__ void __launch_bounds__(NT, OCC)
+__global__ void __launch_bounds__(GGS_DEPTH_SPLIT ? 2 * NT : NT, OCC)
 raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, int B, int N, int H, int W, int nTX,
               int nTiles,
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
               const float* __restrict__ clean, const int* __restrict__ live, int CH, FinFused fin, int simds) {
-    __shared__ int lists[WPB][CAP];   // per-wave strip lists (descending splat index)
+    constexpr bool DS = GGS_DEPTH_SPLIT && MODE == 1 && !SAT;
+    __shared__ int lists[DS ? 2 : WPB][CAP];   // per-wave strip lists (descending splat index)
 
     const int lane = threadIdx.x & 63;
 #if GGS_TIMING
@@ -318,7 +328,12 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     unsigned long long t_cull = 0, t_vis = 0, t_mark = __builtin_amdgcn_s_memtime();
     unsigned n_vis = 0, n_done = 0;     // listed / blended visits
 #endif
+#if GGS_DEPTH_SPLIT
+    const int wib = DS ? 0 : ufirst((int)(threadIdx.x >> 6));  // wave in block (uniform: keeps control on SALU)
+    const int half = DS ? ufirst((int)(threadIdx.x >> 6)) : 0;  // depth split: 0 front, 1 back
+#else
     const int wib = ufirst((int)(threadIdx.x >> 6));  // wave in block (uniform: keeps control on SALU)
+#endif
     // SA loop rounds: the grid is sized for the session's capacity and only the
     // first *live candidates are evaluated; the grid order below is then that of
     // a launch over *live candidates, and the blocks past it exit at once
@@ -368,6 +383,9 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     if (MODE != 0 && dirty) {         // incremental (SA): a strip no changed splat touches
         const int64_t slot = ((int64_t)b * nTiles + t) * 4 + wv;   // keeps the current state's
         if (!dirty[slot]) {                                         // partial, bit for bit
+#if GGS_DEPTH_SPLIT
+            if (DS && half) return;
+#endif
             if (lane == 0) store_partial(partials + slot, clean[t * 4 + wv], FUSED);
             if (FUSED) strip_done(fin, partials, b, nTiles * 4, lane);
             return;
@@ -391,7 +409,23 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 
     const SplatRec* __restrict__ crec = recs + (int64_t)b * N;
     const int4* __restrict__ cbnd = bnds + (int64_t)b * N;
+#if GGS_DEPTH_SPLIT
+    int* __restrict__ list = &lists[0][0] + (wib + half) * CAP;
+    // the splat indices this wave culls: [nlo, nhi) (all of them but with the depth split)
+    const int nlo = DS && half == 0 ? N / 2 : 0, nhi = DS && half == 1 ? N / 2 : N, nr = nhi - nlo;
+    __shared__ int s_cnt[2];
+    int lbase = 0, c0 = 0;            // depth split: this wave's part of the joint list
+#define GGS_NHI nhi
+#define GGS_NLO nlo
+#define GGS_NR nr
+#define GGS_LIST_AT(q) list_at(q)
+#else
     int* __restrict__ list = &lists[0][0] + wib * CAP;
+#define GGS_NHI N
+#define GGS_NLO 0
+#define GGS_NR N
+#define GGS_LIST_AT(q) list[q]
+#endif
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int cnt = 0;
     // every pixel of the strip below SAT_EPS transmittance (wave-uniform)
@@ -415,16 +449,22 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     constexpr int AHEAD = SAT ? GGS_SAT_AHEAD : GGS_CULL_AHEAD;
     static_assert(AHEAD >= 1 && AHEAD <= 4, "cull prefetch depth");
     // issued in chunk order (sched barriers), so each chunk waits vmcnt(AHEAD - 1)
-    int4 bbA = bounds(N - 1 - lane), bbB, bbC, bbD;
-    if constexpr (AHEAD > 1) { __builtin_amdgcn_sched_barrier(0); bbB = bounds(N - 1 - lane - 64); }
-    if constexpr (AHEAD > 2) { __builtin_amdgcn_sched_barrier(0); bbC = bounds(N - 1 - lane - 128); }
-    if constexpr (AHEAD > 3) { __builtin_amdgcn_sched_barrier(0); bbD = bounds(N - 1 - lane - 192); }
+    int4 bbA = bounds(GGS_NHI - 1 - lane), bbB, bbC, bbD;
+    if constexpr (AHEAD > 1) { __builtin_amdgcn_sched_barrier(0); bbB = bounds(GGS_NHI - 1 - lane - 64); }
+    if constexpr (AHEAD > 2) { __builtin_amdgcn_sched_barrier(0); bbC = bounds(GGS_NHI - 1 - lane - 128); }
+    if constexpr (AHEAD > 3) { __builtin_amdgcn_sched_barrier(0); bbD = bounds(GGS_NHI - 1 - lane - 192); }
     int base = 0;                     // first splat (from the back) not yet culled
     // a batch is handed to the blend once it holds more than LIMIT splats; a step
     // adds at most 64 * AHEAD, so the list (CAP) cannot overflow
     constexpr int LIMIT = SAT ? SAT_BATCH - 64 : CAP - 64 * AHEAD;
     static_assert(LIMIT + 64 * AHEAD <= CAP, "cull list capacity");
+#if GGS_DEPTH_SPLIT
+    // (the depth split: one pass, whose barrier both waves reach even with no splats)
+    for (int pass = 0;; ++pass) {
+        if (DS ? pass > 0 : base >= nr) break;
+#else
     while (base < N) {
+#endif
         // wave priority: the load-bound cull issues ahead of other waves' blends (+0.4 %)
         __builtin_amdgcn_s_setprio(CULL_PRIO);
         // --- cull 64 splats (descending index = front-to-back) against the strip:
@@ -432,10 +472,10 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         // splits it into two dependent loads), then a branch-free overlap test
 #define GGS_CULL_CHUNK(BB)                                                                  \
         {                                                                                   \
-            const int i = N - 1 - (base + lane);                                            \
+            const int i = GGS_NHI - 1 - (base + lane);                                      \
             const int4 bb = BB;                                               /* x0 x1 y0 y1 */ \
             if (AHEAD == 1) BB = bounds(i - 64);                                            \
-            const bool hit = (i >= 0) & (bb.w >= ty0) & (bb.z <= ty1) & (bb.y >= sx0) & (bb.x <= sx0 + 15); \
+            const bool hit = (i >= GGS_NLO) & (bb.w >= ty0) & (bb.z <= ty1) & (bb.y >= sx0) & (bb.x <= sx0 + 15); \
             /* deeper: reload after the test, into the registers just read */              \
             if (AHEAD > 1) BB = bounds(i - 64 * AHEAD);                                     \
             const uint64_t m = __ballot(hit);                                               \
@@ -445,16 +485,27 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         }
         if constexpr (AHEAD == 1) {
             GGS_CULL_CHUNK(bbA)
-            if (cnt <= LIMIT && base < N) continue;
+            if (cnt <= LIMIT && base < GGS_NR) continue;
         } else {
             do {                                  // past N: no hits (i < 0), clamped loads
                 GGS_CULL_CHUNK(bbA)
                 GGS_CULL_CHUNK(bbB)
                 if constexpr (AHEAD > 2) GGS_CULL_CHUNK(bbC)
                 if constexpr (AHEAD > 3) GGS_CULL_CHUNK(bbD)
-            } while (cnt <= LIMIT && base < N);
+            } while (cnt <= LIMIT && base < GGS_NR);
         }
 #undef GGS_CULL_CHUNK
+#if GGS_DEPTH_SPLIT
+        if constexpr (DS) {           // N / 2 <= SAT_MIN_SPLATS / 2 < LIMIT: culled in one batch
+            static_assert(!DS || SAT_MIN_SPLATS / 2 + 64 * AHEAD <= CAP, "depth split: one cull batch");
+            if (lane == 0) s_cnt[half] = cnt;
+            __syncthreads();
+            c0 = ufirst(s_cnt[0]);
+            const int total = c0 + ufirst(s_cnt[1]), hs = (total + 1) >> 1;
+            lbase = half ? hs : 0;
+            cnt = half ? total - hs : hs;
+        }
+#endif
         if (cnt == 0) continue;       // (base >= N: the loop ends)
         __builtin_amdgcn_s_setprio(0);
 #if GGS_TIMING
@@ -468,7 +519,19 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         // (byte offsets: the record load takes the readlane result as its
         //  32-bit SGPR offset; past the list end it reloads a listed record)
         const char* __restrict__ cbase = reinterpret_cast<const char*>(crec);
-        int offv = list[min(lane, cnt - 1)];
+#if GGS_DEPTH_SPLIT
+        // the joint list of the depth split: lists[0][0, c0) then lists[1]
+        auto list_at = [&](int q) __attribute__((always_inline)) {
+            if constexpr (DS) {
+                q += lbase;
+                const int a0 = lists[0][min(q, CAP - 1)], a1 = lists[1][max(q - c0, 0)];
+                return q < c0 ? a0 : a1;
+            } else {
+                return list[q];
+            }
+        };
+#endif
+        int offv = GGS_LIST_AT(min(lane, cnt - 1));
         // one (splat, strip) visit: cull-list record s -> the strip's accumulators
         auto visit = [&](const SplatRec& s) __attribute__((always_inline)) {
 #if GGS_TIMING
@@ -709,11 +772,11 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         SplatRec ra = load_at(0);
         int jr = 63;                  // last j before the next 64 offsets are needed
         for (int j = 0;;) {
-            if (__builtin_expect(j == jr, 0)) { jr += 64; offv = list[min(j + 1 + lane, cnt - 1)]; }
+            if (__builtin_expect(j == jr, 0)) { jr += 64; offv = GGS_LIST_AT(min(j + 1 + lane, cnt - 1)); }
             const SplatRec rb = load_at(j + 1);
             visit(ra);
             if (++j >= cnt) break;
-            if (__builtin_expect(j == jr, 0)) { jr += 64; offv = list[min(j + 1 + lane, cnt - 1)]; }
+            if (__builtin_expect(j == jr, 0)) { jr += 64; offv = GGS_LIST_AT(min(j + 1 + lane, cnt - 1)); }
             ra = load_at(j + 1);
             visit(rb);
             if (++j >= cnt) break;
@@ -737,6 +800,45 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         { GGS_TMARK(now); t_vis += now - t_mark; t_mark = now; }
 #endif
     }
+
+#undef GGS_NHI
+#undef GGS_NLO
+#undef GGS_NR
+#undef GGS_LIST_AT
+#if GGS_DEPTH_SPLIT
+    if constexpr (DS) {
+        // wave 1 hands its (C, T) to wave 0 through the lists' 8 KB, four pairs
+        // (32 floats per lane) at a time; wave 0 composes front over back
+        float* __restrict__ xs = reinterpret_cast<float*>(&lists[0][0]);
+        __syncthreads();              // both waves done with the lists
+#define GGS_XW(k, k0)                                                                  \
+        if ((k) < NPK) {                                                               \
+            float* x_ = xs + 8 * ((k) - (k0)) * 64 + lane;                             \
+            x_[0] = P_R##k.x; x_[64] = P_R##k.y; x_[128] = P_G##k.x; x_[192] = P_G##k.y;   \
+            x_[256] = P_B##k.x; x_[320] = P_B##k.y; x_[384] = P_T##k.x; x_[448] = P_T##k.y; \
+        }
+#define GGS_XR(k, k0)                                                                  \
+        if ((k) < NPK) {                                                               \
+            const float* x_ = xs + 8 * ((k) - (k0)) * 64 + lane;                       \
+            const f2_t rb_ = {x_[0], x_[64]}, gb_ = {x_[128], x_[192]};                \
+            const f2_t bb_ = {x_[256], x_[320]}, tb_ = {x_[384], x_[448]};             \
+            P_R##k = fma2(P_T##k, rb_, P_R##k);                                        \
+            P_G##k = fma2(P_T##k, gb_, P_G##k);                                        \
+            P_B##k = fma2(P_T##k, bb_, P_B##k);                                        \
+            P_T##k = P_T##k * tb_;                                                     \
+        }
+#define GGS_XCHUNK(k0, k1, k2, k3)                                                     \
+        if (half) { GGS_XW(k0, k0) GGS_XW(k1, k0) GGS_XW(k2, k0) GGS_XW(k3, k0) }      \
+        __syncthreads();                                                               \
+        if (!half) { GGS_XR(k0, k0) GGS_XR(k1, k0) GGS_XR(k2, k0) GGS_XR(k3, k0) }      \
+        __syncthreads();
+        GGS_XCHUNK(0, 1, 2, 3) GGS_XCHUNK(4, 5, 6, 7) GGS_XCHUNK(8, 9, 10, 11) GGS_XCHUNK(12, 13, 14, 15)
+#undef GGS_XCHUNK
+#undef GGS_XR
+#undef GGS_XW
+        if (half) return;
+    }
+#endif
 
     // --- epilogue ---------------------------------------------------------------
     float R[RG], G[RG], Bl[RG], T[RG];
@@ -1059,17 +1161,18 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const i
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
+    const bool sat = N > SAT_MIN_SPLATS;
+    const dim3 block_f(GGS_DEPTH_SPLIT && !sat ? 2 * NT : NT);   // fitness instances (depth split: 2 waves)
     const int CH = raster_chunk(N);
     const FinFused ff = (mode != 0 && fin) ? *fin : FinFused{};
-    const int simds = raster_simds();
+    const int simds = GGS_DEPTH_SPLIT ? 0 : raster_simds();
     // FUSED is a template parameter, so the instances without the fold carry none
     // of its code (a runtime test left the SA raster 1 % slower than round 3's)
 #define GGS_RASTER(M, S, F)                                                                    \
-    hipLaunchKernelGGL((raster_kernel<M, S, F>), grid, block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
+    hipLaunchKernelGGL((raster_kernel<M, S, F>), grid, (M) ? block_f : block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
                        bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH, ff, simds)
     // the saturation check only where strip lists can grow long (N > SAT_MIN_SPLATS);
     // at the bench's 256 splats the kernel without it is the faster code (+1.6 %)
-    const bool sat = N > SAT_MIN_SPLATS;
     if (mode == 0) { if (!sat) GGS_RASTER(0, false, false); else GGS_RASTER(0, true, false); }   // image
     else if (!ff.ctr) { if (!sat) GGS_RASTER(1, false, false); else GGS_RASTER(1, true, false); }   // fitness
     else { if (!sat) GGS_RASTER(1, false, true); else GGS_RASTER(1, true, true); }  // + folded finalize
