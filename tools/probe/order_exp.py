@@ -3,6 +3,7 @@ rtime.py's 2048^2 SA configs from the model's per-strip costs (sched_model.py) o
 the exact populations rtime.py renders, with the model's makespan per order.
 
     python tools/probe/order_exp.py --pop 2      -> tools/probe/orders/sa2_{lpt,centre}.bin
+    python tools/probe/order_exp.py --pop 24 --size 512 --splats 512 --tag ga24
 """
 import argparse
 import os
@@ -20,6 +21,7 @@ ap.add_argument("--pop", type=int, default=2)
 ap.add_argument("--size", type=int, default=2048)
 ap.add_argument("--splats", type=int, default=4096)
 ap.add_argument("--same", action="store_true", help="rtime.py --same populations")
+ap.add_argument("--tag", default="")
 a = ap.parse_args()
 import bench  # noqa: E402
 bench.H = bench.W = a.size
@@ -36,4 +38,4 @@ for name, o in orders.items():
     ms = [M.simulate(M.group_order_blocks(c, list(o))) for c in costs]
     ideal = [c.sum() / 1024 for c in costs]
     print(f"{name:8s} model makespan x ideal " + " ".join("%.3f" % (m / i) for m, i in zip(ms, ideal)))
-    o.astype(np.int32).tofile(os.path.join(HERE, "orders", f"sa{a.pop}{'same' if a.same else ''}_{name}.bin"))
+    o.astype(np.int32).tofile(os.path.join(HERE, "orders", f"{a.tag or 'sa%d' % a.pop}{'same' if a.same else ''}_{name}.bin"))
