@@ -13,7 +13,7 @@
     (defined(GGS_NOPLAN) || defined(GGS_TIMING) || defined(GGS_VTIMING) || defined(GGS_SATURATE) || \
      defined(GGS_SAT_EVERY) || defined(GGS_SAT_BATCH) || defined(GGS_SAT_AHEAD) ||             \
      defined(GGS_CULL_AHEAD) || defined(GGS_CHUNK_MB) || defined(GGS_NO_RATIO_CLAMP) ||               \
-     defined(GGS_DEPTH_SPLIT))
+     defined(GGS_DEPTH_SPLIT) || defined(GGS_TILE_H))
 #error "GGS_* diagnostic knobs are for the probe build only: make probe PROBE=\"-D...\""
 #endif
 #ifdef GGS_PROBE_BUILD

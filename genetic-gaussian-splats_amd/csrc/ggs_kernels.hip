@@ -94,7 +94,10 @@ prep_kernel(const float* __restrict__ genomes, int64_t S, int C, int H, int W, f
 // raster
 // ---------------------------------------------------------------------------
 constexpr int TILE = 64;          // tile width (pixels): 4 strips of 16 columns
-constexpr int TILE_H = 128;       // tile height: one wave covers a 16 x 128 strip, 32 pixels per lane
+#ifndef GGS_TILE_H
+#define GGS_TILE_H 128            // probe build only: other strip heights (multiples of 8)
+#endif
+constexpr int TILE_H = GGS_TILE_H;  // tile height: one wave covers a 16 x 128 strip, 32 pixels per lane
                                   // (round 1: 64 rows at 5 waves/SIMD 0.260 ms, 96 at 4: 0.249, 128 at 3: 0.249)
 constexpr int RG = TILE_H / 4;    // row groups per lane (rows r, r+4, ...)
 constexpr int NPK = RG / 2;       // packed row-group pairs per lane
@@ -750,12 +753,12 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #undef GGS_XMID
         x15:
         xlast:
-            switch (kB) {
+            switch (kB == NPK ? 16 : kB) {   // (case 16: pair NPK-1 ran unmasked)
 #define GGS_LAST(k) case k: if (k < NPK) GGS_PK(k, true); break;
                 GGS_LAST(1) GGS_LAST(2) GGS_LAST(3) GGS_LAST(4) GGS_LAST(5) GGS_LAST(6)
                 GGS_LAST(7) GGS_LAST(8) GGS_LAST(9) GGS_LAST(10) GGS_LAST(11) GGS_LAST(12)
                 GGS_LAST(13) GGS_LAST(14) GGS_LAST(15)
-                case NPK: break;              // pair 15 ran unmasked (x14)
+                case 16: break;               // kB == NPK: the last pair ran unmasked
 #undef GGS_LAST
                 default: __builtin_unreachable();
             }
