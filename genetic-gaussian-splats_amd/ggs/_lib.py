@@ -149,8 +149,12 @@ def _share_hip_runtime_with_torch() -> None:
 
 def preload_rccl() -> None:
     """Same rule for RCCL (ggs_comm_*): PyTorch bundles its own librccl with the
-    SONAME of /opt/rocm's; load torch's first so libggs's dlopen finds the copy
-    torch.distributed uses.  Called before the first communicator is made."""
+    SONAME of /opt/rocm's, so libggs's dlopen must find the copy torch.distributed
+    uses.  Called before the first communicator is made.  torch itself is imported
+    here, not just its librccl: a process that initialised RCCL and imported torch
+    only afterwards aborted at interpreter exit ("double free or corruption", after
+    every call had returned; tools/probe/exit_bisect.sh: tests/test_gpu_comm.py then
+    test_gpu_parity.py's torch tests), while torch imported first never did."""
     if os.environ.get("GGS_HIP_RUNTIME", "") == "system":
         return
     import importlib.util
@@ -160,6 +164,11 @@ def preload_rccl() -> None:
         return
     if spec is None or not spec.submodule_search_locations:
         return
+    try:
+        import torch  # noqa: F401  (loads its librccl as well)
+        return
+    except Exception:  # noqa: BLE001 — a broken torch install: bind its librccl only
+        pass
     p = os.path.join(list(spec.submodule_search_locations)[0], "lib", "librccl.so")
     if os.path.exists(p):
         C.CDLL(p, mode=C.RTLD_GLOBAL)
