@@ -168,7 +168,7 @@ struct DevCtx {
     std::vector<std::unique_ptr<Workspace>> ws;
     // host-API staging
     DevBuf gen, out, target, mask;
-    PinBuf h_gen, h_out;
+    PinBuf h_out;                  // the fitness scalars (render and genomes go straight to / from the caller)
     uint64_t target_key = 0, mask_key = 0;
     size_t target_bytes = 0, mask_bytes = 0;
 };
@@ -286,11 +286,6 @@ int init_locked(int max_devices) {
     for (int d = 0; d < n; ++d) g_active.push_back(d);
     g_inited = true;
     return n;
-}
-
-int lazy_init() {
-    std::lock_guard<std::mutex> lk(g_mu);
-    return init_locked(0);
 }
 
 // Context of device d, created on first use (one stream per device).  g_mu held.
@@ -550,7 +545,7 @@ void ggs_shutdown(void) {
         }
         for (DevBuf* b : {&c->gen, &c->out, &c->target, &c->mask})
             if (b->p) (void)hipFree(b->p);
-        for (PinBuf* b : {&c->h_gen, &c->h_out})
+        for (PinBuf* b : {&c->h_out})
             if (b->p) (void)hipHostFree(b->p);
         (void)hipStreamDestroy(c->stream);
     }
@@ -696,12 +691,12 @@ int fitness_one_device_speculative(DevCtx* c, const float* genomes_axes, int64_t
     if ((rc = ensure(c->out, sizeof(float) * (size_t)B, st))) return rc;
     if ((rc = ensure_pinned(c->h_out, sizeof(float) * (size_t)B))) return rc;
     if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
-    if ((rc = ensure_pinned(c->h_gen, std::max<size_t>(gbytes, 4)))) return rc;
-    GGS_HIP(hipStreamSynchronize(st));  // pinned staging may still feed a previous copy
-    if (gbytes) {
-        memcpy(c->h_gen.p, genomes_axes, gbytes);
-        GGS_HIP(hipMemcpyAsync(c->gen.p, c->h_gen.p, gbytes, hipMemcpyHostToDevice, st));
-    }
+    GGS_HIP(hipStreamSynchronize(st));  // the previous call's work is done with c->gen
+    // straight from the caller's (pageable) array: the runtime's own staged copy
+    // beat a memcpy into our pinned buffer + its upload by ~25 us per call at
+    // 512^2/256/128 (1.18 MB: 240 -> 215 us per call; docs/EXPERIMENTS.md §15).  The
+    // array stays valid for the whole call, which syncs before returning.
+    if (gbytes) GGS_HIP(hipMemcpyAsync(c->gen.p, genomes_axes, gbytes, hipMemcpyHostToDevice, st));
     const uint64_t mkey_c = mask_hw ? c->mask_key : 0;
     auto evaluate = [&](uint64_t tk, uint64_t mk) {
         int r = run_fitness(c, st, (const float*)c->gen.p, B, N, C, (const float*)c->target.p,
@@ -793,12 +788,9 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
         }
         const size_t gbytes = sizeof(float) * row * (size_t)nb;
         if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
-        if ((rc = ensure_pinned(c->h_gen, std::max<size_t>(gbytes, 4)))) return rc;
-        GGS_HIP(hipStreamSynchronize(st));  // pinned staging may still feed a previous copy
-        if (gbytes) {
-            memcpy(c->h_gen.p, genomes_axes + row * b0, gbytes);
-            GGS_HIP(hipMemcpyAsync(c->gen.p, c->h_gen.p, gbytes, hipMemcpyHostToDevice, st));
-        }
+        GGS_HIP(hipStreamSynchronize(st));  // the previous call's work is done with c->gen
+        if (gbytes)                         // straight from the caller's array (see above)
+            GGS_HIP(hipMemcpyAsync(c->gen.p, genomes_axes + row * b0, gbytes, hipMemcpyHostToDevice, st));
         if ((rc = run_fitness(c, st, (const float*)c->gen.p, nb, N, C, (const float*)c->target.p,
                               mask_hw ? (const float*)c->mask.p : nullptr, mode, boost_beta, H, W,
                               k_sigma, (float*)c->out.p + (gather ? b0 : 0),
@@ -861,16 +853,13 @@ int ggs_render(const float* genomes, int64_t B, int32_t N, int32_t C, int32_t H,
         const size_t gbytes = sizeof(float) * row * (size_t)nb;
         if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
         if ((rc = ensure(c->out, img1 * nb, st))) return rc;
-        if ((rc = ensure_pinned(c->h_gen, std::max<size_t>(gbytes, 4)))) return rc;
-        if ((rc = ensure_pinned(c->h_out, img1 * nb))) return rc;
         GGS_HIP(hipStreamSynchronize(st));
-        if (gbytes) {
-            memcpy(c->h_gen.p, genomes + row * b0, gbytes);
-            GGS_HIP(hipMemcpyAsync(c->gen.p, c->h_gen.p, gbytes, hipMemcpyHostToDevice, st));
-        }
+        // straight from / to the caller's (pageable) arrays, as the fitness host API
+        if (gbytes)
+            GGS_HIP(hipMemcpyAsync(c->gen.p, genomes + row * b0, gbytes, hipMemcpyHostToDevice, st));
         if ((rc = run_render(c, st, (const float*)c->gen.p, nb, N, C, H, W, k_sigma, bgp, (float*)c->out.p)))
             return rc;
-        GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, img1 * nb, hipMemcpyDeviceToHost, st));
+        GGS_HIP(hipMemcpyAsync((char*)out_bhw3 + img1 * b0, c->out.p, img1 * nb, hipMemcpyDeviceToHost, st));
     }
     for (int d = 0; d < nd; ++d) {
         DevCtx* c = cs[d];
@@ -879,7 +868,6 @@ int ggs_render(const float* genomes, int64_t B, int32_t N, int32_t C, int32_t H,
         if (nb == 0) continue;
         DeviceGuard dg(c->dev);
         GGS_HIP(hipStreamSynchronize(c->stream));
-        memcpy((char*)out_bhw3 + img1 * b0, c->h_out.p, img1 * nb);
     }
     return GGS_OK;
 }
