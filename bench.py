@@ -864,6 +864,14 @@ def run(args, world, rank, local_rank, distributed):
                     "note": "24 FLOP per AABB pair the reference's per-pixel loop would execute "
                             "(SURVEY.md §8d); the row recurrence executes fewer, so this ratio can "
                             "exceed 1 and is not a roofline fraction"}}
+    # what the collective ran on, as RCCL itself reports it (every rank takes part
+    # in the host all-gather of (rank, device) pairs), and the runtimes' provenance
+    rccl_ranks = rank_devices = None
+    if comms:
+        n_r, r_r, d_r = comms[0].info()
+        rccl_ranks = n_r
+        rank_devices = [[int(a), int(b)] for a, b in comms[0].allgather_host([float(r_r), float(d_r)])]
+    runtime = ggs.runtime_info()
     if rank == 0:
         line = {
             "metric": METRIC if headline else
@@ -893,7 +901,8 @@ def run(args, world, rank, local_rank, distributed):
                        "H": H, "W": W, "splats": N_SPLATS, "pop_per_gpu": POP,
                        "global_batch": global_batch, "parallelism": f"dp{world} (candidate shards)",
                        "fitness_gather": (GATHER if comms else None),
-                       "rccl_ranks": (world if comms else None)},
+                       "rccl_ranks": rccl_ranks,            # ncclCommCount of this run's communicator
+                       "rank_devices": rank_devices},       # [ncclCommUserRank, ncclCommCuDevice] per rank
             "timing": {"passes": passes, "statistic": "median pass of K steps (max over ranks per pass)",
                        "measured_s": round(elapsed * passes, 3)},
             "gsplat_pixels_per_s": round(value * N_SPLATS * H * W / 1e9, 2),
@@ -913,6 +922,7 @@ def run(args, world, rank, local_rank, distributed):
                                    f"so each event figure carries the pair's overhead and the launch gap; "
                                    f"kernels_ms_rocprof is the committed trace of the same binary"),
             "hip_runtime": _mapped("libamdhip64"),
+            "runtime": runtime,                              # ggs_runtime_info: HIP + RCCL paths, versions, one tree
             "torch_loaded": "torch" in sys.modules,
             "cpu_baseline": cpu,
         }

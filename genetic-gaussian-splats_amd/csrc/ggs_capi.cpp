@@ -163,6 +163,7 @@ int ensure_tile_order(Workspace* w, int H, int W, hipStream_t st) {
 
 struct DevCtx {
     int dev = 0;
+    int simds = 0;                 // CUs x 4 of dev (single-round raster ordering)
     hipStream_t stream = nullptr;  // library-owned stream for the host API
     std::mutex mu;
     std::vector<std::unique_ptr<Workspace>> ws;
@@ -179,16 +180,17 @@ std::vector<int> g_active;                    // devices the host API fans out o
 bool g_inited = false;
 
 // ---- profiling ----------------------------------------------------------------
+constexpr int kProfKernels = 4;
 struct ProfRec {
-    int kernel;  // 0 prep, 1 raster, 2 finalize
+    int kernel;  // 0 prep, 1 raster, 2 finalize, 3 lpt (single-round packing)
     hipEvent_t a, b;
 };
 std::mutex g_prof_mu;
 bool g_prof_on = false;
 std::vector<ProfRec> g_prof_pending;
-double g_prof_ms[3] = {0, 0, 0};
-int64_t g_prof_n[3] = {0, 0, 0};
-const char* const kKernelNames[3] = {"prep", "raster", "finalize"};
+double g_prof_ms[kProfKernels] = {};
+int64_t g_prof_n[kProfKernels] = {};
+const char* const kKernelNames[kProfKernels] = {"prep", "raster", "finalize", "lpt"};
 
 struct ProfScope {
     bool on = false;
@@ -227,10 +229,10 @@ void prof_drain_locked() {
 }
 
 // raster (MODE 1) + finalize of B candidates: one launch when `fuse` (and allowed).
-int raster_fitness(hipStream_t st, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
+int raster_fitness(hipStream_t st, int simds, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                    const float4* plan, float* partials, const float* wpartials, int mode, const int* order,
                    DevBuf& ctr, float* out, bool fuse, const unsigned char* dirty = nullptr,
-                   const float* clean = nullptr) {
+                   const float* clean = nullptr, const int* blk_map = nullptr) {
     const float bg[3] = {1.f, 1.f, 1.f};  // fitness renders with the default background (fitness.py:15)
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
@@ -249,12 +251,13 @@ int raster_fitness(hipStream_t st, const SplatRec* recs, const int4* bnds, int B
         ff.mode = mode;
         ProfScope ps(st, 1);
         GGS_HIP(launch_raster(st, 1, recs, bnds, B, N, H, W, bg, nullptr, plan, partials, order, dirty, clean,
-                              nullptr, &ff));
+                              nullptr, &ff, simds, blk_map));
         return GGS_OK;
     }
     {
         ProfScope ps(st, 1);
-        GGS_HIP(launch_raster(st, 1, recs, bnds, B, N, H, W, bg, nullptr, plan, partials, order, dirty, clean));
+        GGS_HIP(launch_raster(st, 1, recs, bnds, B, N, H, W, bg, nullptr, plan, partials, order, dirty, clean,
+                              nullptr, nullptr, simds, blk_map));
     }
     ProfScope ps(st, 2);
     GGS_HIP(launch_finalize(st, partials, wpartials, B, nTiles, mode, H, W, out));
@@ -272,6 +275,45 @@ struct DeviceGuard {
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
+
+// Host API: every stream this call has queued work on — copies from or into the
+// caller's arrays included — is synchronised before the call returns, on error
+// returns too, so the caller's arrays are never touched after the call
+// (include/ggs.h: pointers are used only during the call).  Declared after the
+// context locks, so it drains while they are held.
+struct StreamDrain {
+    std::vector<std::pair<int, hipStream_t>> s;
+    void add(int dev, hipStream_t st) {
+        for (auto& x : s)
+            if (x.second == st) return;
+        s.emplace_back(dev, st);
+    }
+    // returns the first failure (GGS_OK if none) and empties the list
+    int drain() {
+        int rc = GGS_OK;
+        for (auto& x : s) {
+            DeviceGuard dg(x.first);
+            const hipError_t e = hipStreamSynchronize(x.second);
+            if (e != hipSuccess && rc == GGS_OK)
+                rc = fail(GGS_EHIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+        }
+        s.clear();
+        return rc;
+    }
+    ~StreamDrain() {
+        const std::string keep = t_err;          // an error return keeps its own message
+        (void)drain();
+        t_err = keep;
+    }
+};
+
+// Test hook (GGS_TEST_FAIL_AFTER_ENQUEUE=d): the host API fails with GGS_EHIP
+// right after queueing device d's work (d from 1), as a HIP failure on a later
+// shard would; read per call.
+bool inject_fail_after(int d) {
+    const char* v = getenv("GGS_TEST_FAIL_AFTER_ENQUEUE");
+    return v && atoi(v) == d;
+}
 
 int init_locked(int max_devices) {
     if (g_inited) return (int)g_ctx.size();
@@ -297,6 +339,7 @@ int ctx_locked(int d, DevCtx** out) {
         c->dev = d;
         DeviceGuard dg(d);
         GGS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->simds = device_simds(d);
         g_ctx[d] = std::move(c);
     }
     *out = g_ctx[d].get();
@@ -424,7 +467,7 @@ int run_fitness_planned(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B
         ProfScope ps(st, 0);
         GGS_HIP(launch_prep(st, true, d_gen, B * N, C, H, W, k, recs, (int4*)w->bnds.p, nullptr, nullptr, nullptr));
     }
-    return raster_fitness(st, recs, (const int4*)w->bnds.p, (int)B, N, H, W, plan, (float*)w->partials.p,
+    return raster_fitness(st, c->simds, recs, (const int4*)w->bnds.p, (int)B, N, H, W, plan, (float*)w->partials.p,
                           wpartials, mode, (const int*)w->order.p, w->fctr, d_out, fitness_api_fold());
 }
 
@@ -444,7 +487,7 @@ int run_render(DevCtx* c, hipStream_t st, const float* d_gen, int64_t B, int N, 
     {
         ProfScope ps(st, 1);
         GGS_HIP(launch_raster(st, 0, recs, (const int4*)w->bnds.p, (int)B, N, H, W, bg, d_img, nullptr, nullptr,
-                              (const int*)w->order.p));
+                              (const int*)w->order.p, nullptr, nullptr, nullptr, nullptr, c->simds));
     }
     return GGS_OK;
 }
@@ -692,6 +735,8 @@ int fitness_one_device_speculative(DevCtx* c, const float* genomes_axes, int64_t
     if ((rc = ensure_pinned(c->h_out, sizeof(float) * (size_t)B))) return rc;
     if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
     GGS_HIP(hipStreamSynchronize(st));  // the previous call's work is done with c->gen
+    StreamDrain drain;                  // after the context lock: drained on every return
+    drain.add(c->dev, st);
     // straight from the caller's (pageable) array: the runtime's own staged copy
     // beat a memcpy into our pinned buffer + its upload by ~25 us per call at
     // 512^2/256/128 (1.18 MB: 240 -> 215 us per call; docs/EXPERIMENTS.md §15).  The
@@ -707,10 +752,12 @@ int fitness_one_device_speculative(DevCtx* c, const float* genomes_axes, int64_t
         return GGS_OK;
     };
     if ((rc = evaluate(c->target_key, mkey_c))) return rc;
+    if (inject_fail_after(1)) return fail(GGS_EHIP, "injected failure after device 1's work (test hook)");
     const uint64_t tkey = hash_bytes(target_hw3, tbytes);      // while the GPU runs
     const uint64_t mkey = mask_hw ? hash_bytes(mask_hw, mbytes) : 0;
-    GGS_HIP(hipStreamSynchronize(st));
+    if ((rc = drain.drain())) return rc;
     if (tkey != c->target_key || mkey != mkey_c) {            // changed: redo with the new inputs
+        drain.add(c->dev, st);
         if (tkey != c->target_key) {
             GGS_HIP(hipMemcpyAsync(c->target.p, target_hw3, tbytes, hipMemcpyHostToDevice, st));
             c->target_key = tkey;
@@ -720,7 +767,7 @@ int fitness_one_device_speculative(DevCtx* c, const float* genomes_axes, int64_t
             c->mask_key = mkey;
         }
         if ((rc = evaluate(tkey, mkey))) return rc;
-        GGS_HIP(hipStreamSynchronize(st));
+        if ((rc = drain.drain())) return rc;
     }
     memcpy(out_B, c->h_out.p, sizeof(float) * (size_t)B);
     *done = 1;
@@ -760,6 +807,7 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
 
     std::vector<std::unique_lock<std::mutex>> locks;
     for (int d = 0; d < nd; ++d) locks.emplace_back(cs[d]->mu);
+    StreamDrain drain;                  // every stream given work is synchronised on any return
     // enqueue on every device, then gather (nd > 1) and wait
     for (int d = 0; d < nd; ++d) {
         DevCtx* c = cs[d];
@@ -789,6 +837,7 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
         const size_t gbytes = sizeof(float) * row * (size_t)nb;
         if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
         GGS_HIP(hipStreamSynchronize(st));  // the previous call's work is done with c->gen
+        drain.add(c->dev, st);
         if (gbytes)                         // straight from the caller's array (see above)
             GGS_HIP(hipMemcpyAsync(c->gen.p, genomes_axes + row * b0, gbytes, hipMemcpyHostToDevice, st));
         if ((rc = run_fitness(c, st, (const float*)c->gen.p, nb, N, C, (const float*)c->target.p,
@@ -798,6 +847,7 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
             return rc;
         if (!gather)
             GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, sizeof(float) * nb, hipMemcpyDeviceToHost, st));
+        if (inject_fail_after(d + 1)) return fail(GGS_EHIP, "injected failure after device %d's work (test hook)", d + 1);
     }
     if (gather) {
         // north_star: one RCCL gather of the shards' fitness scalars (in place, every
@@ -811,19 +861,16 @@ int ggs_fitness(const float* genomes_axes, int64_t B, int32_t N, int32_t C, cons
             sts.push_back(c->stream);
             bufs.push_back((float*)c->out.p);
         }
+        for (DevCtx* c : cs) drain.add(c->dev, c->stream);    // devices without candidates gather too
         if ((rc = comm_group_allgather_inplace(comms.data(), nd, sts.data(), bufs.data(), per))) return rc;
         DeviceGuard dg(cs[0]->dev);
         GGS_HIP(hipMemcpyAsync(cs[0]->h_out.p, cs[0]->out.p, sizeof(float) * B, hipMemcpyDeviceToHost,
                                cs[0]->stream));
-        for (int d = nd - 1; d >= 0; --d) {     // every device's gather done (the first: and its D2H)
-            DeviceGuard dg2(cs[d]->dev);
-            GGS_HIP(hipStreamSynchronize(cs[d]->stream));
-        }
+        if ((rc = drain.drain())) return rc;    // every device's gather done (the first: and its D2H)
         memcpy(out_B, cs[0]->h_out.p, sizeof(float) * B);
         return GGS_OK;
     }
-    DeviceGuard dg(cs[0]->dev);
-    GGS_HIP(hipStreamSynchronize(cs[0]->stream));
+    if ((rc = drain.drain())) return rc;
     memcpy(out_B, cs[0]->h_out.p, sizeof(float) * B);
     return GGS_OK;
 }
@@ -843,6 +890,10 @@ int ggs_render(const float* genomes, int64_t B, int32_t N, int32_t C, int32_t H,
     const size_t img1 = sizeof(float) * 3 * (size_t)H * W;
     std::vector<std::unique_lock<std::mutex>> locks;
     for (int d = 0; d < nd; ++d) locks.emplace_back(cs[d]->mu);
+    StreamDrain drain;                  // every stream given work is synchronised on any return
+    // uploads and renders on every device first, then the image copies: a D2H into
+    // pageable memory may run synchronously, and queued before the next device's
+    // upload it would serialise the fan-out
     for (int d = 0; d < nd; ++d) {
         DevCtx* c = cs[d];
         int64_t b0, nb;
@@ -854,12 +905,13 @@ int ggs_render(const float* genomes, int64_t B, int32_t N, int32_t C, int32_t H,
         if ((rc = ensure(c->gen, std::max<size_t>(gbytes, 4), st))) return rc;
         if ((rc = ensure(c->out, img1 * nb, st))) return rc;
         GGS_HIP(hipStreamSynchronize(st));
+        drain.add(c->dev, st);
         // straight from / to the caller's (pageable) arrays, as the fitness host API
         if (gbytes)
             GGS_HIP(hipMemcpyAsync(c->gen.p, genomes + row * b0, gbytes, hipMemcpyHostToDevice, st));
         if ((rc = run_render(c, st, (const float*)c->gen.p, nb, N, C, H, W, k_sigma, bgp, (float*)c->out.p)))
             return rc;
-        GGS_HIP(hipMemcpyAsync((char*)out_bhw3 + img1 * b0, c->out.p, img1 * nb, hipMemcpyDeviceToHost, st));
+        if (inject_fail_after(d + 1)) return fail(GGS_EHIP, "injected failure after device %d's work (test hook)", d + 1);
     }
     for (int d = 0; d < nd; ++d) {
         DevCtx* c = cs[d];
@@ -867,9 +919,9 @@ int ggs_render(const float* genomes, int64_t B, int32_t N, int32_t C, int32_t H,
         shard(B, nd, d, &b0, &nb);
         if (nb == 0) continue;
         DeviceGuard dg(c->dev);
-        GGS_HIP(hipStreamSynchronize(c->stream));
+        GGS_HIP(hipMemcpyAsync((char*)out_bhw3 + img1 * b0, c->out.p, img1 * nb, hipMemcpyDeviceToHost, c->stream));
     }
-    return GGS_OK;
+    return drain.drain();
 }
 
 static int stage_call(bool encode, const float* in, int64_t S, int32_t C, int32_t H, int32_t W, float k,
@@ -945,6 +997,33 @@ int ggs_detmath_eval(int32_t fn, const float* x, const float* y, int64_t n, floa
     return GGS_OK;
 }
 
+int ggs_lpt_pack(const int32_t* costs, int32_t n, int32_t simds, int32_t cost_add, int32_t* map) {
+    if (n < 0 || (n > 0 && (!costs || !map)) || simds < 1)
+        return fail(GGS_EINVAL, "ggs_lpt_pack: need n >= 0, costs, map and simds >= 1");
+    if (n > 0 && !(n > 2 * simds && n <= 3 * simds && n <= LPT_MAX))
+        return fail(GGS_EINVAL, "ggs_lpt_pack: n = %d strips is not one round of 2-3 waves on %d SIMDs (n <= %d)", n,
+                    simds, LPT_MAX);
+    if (n == 0) return GGS_OK;
+    int rc;
+    std::vector<DevCtx*> cs;
+    if ((rc = active_ctxs(1, &cs))) return rc;
+    DevCtx* c = cs[0];
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->dev);
+    struct Scratch {
+        void* p = nullptr;
+        ~Scratch() { if (p) (void)hipFree(p); }
+    } dc, dm;
+    const size_t nb = sizeof(int) * (size_t)n;
+    GGS_HIP(hipMalloc(&dc.p, nb));
+    GGS_HIP(hipMalloc(&dm.p, nb));
+    GGS_HIP(hipMemcpy(dc.p, costs, nb, hipMemcpyHostToDevice));
+    GGS_HIP(launch_lpt(c->stream, (const int*)dc.p, n, simds, cost_add, (int*)dm.p));
+    GGS_HIP(hipStreamSynchronize(c->stream));
+    GGS_HIP(hipMemcpy(map, dm.p, nb, hipMemcpyDeviceToHost));
+    return GGS_OK;
+}
+
 int ggs_profile_enable(int32_t on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;
@@ -954,20 +1033,20 @@ int ggs_profile_enable(int32_t on) {
 int ggs_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     prof_drain_locked();
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < kProfKernels; ++k) {
         if (kernel && strcmp(kernel, kKernelNames[k]) == 0) {
             if (total_ms) *total_ms = g_prof_ms[k];
             if (launches) *launches = g_prof_n[k];
             return GGS_OK;
         }
     }
-    return fail(GGS_EINVAL, "unknown kernel name '%s' (prep|raster|finalize)", kernel ? kernel : "(null)");
+    return fail(GGS_EINVAL, "unknown kernel name '%s' (prep|raster|finalize|lpt)", kernel ? kernel : "(null)");
 }
 
 void ggs_profile_reset(void) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     prof_drain_locked();
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < kProfKernels; ++k) {
         g_prof_ms[k] = 0;
         g_prof_n[k] = 0;
     }
@@ -998,6 +1077,12 @@ struct GaSession {
     int ocur = 0;                  // off[ocur]: the offspring evaluated last
     bool pending = false;          // their survivors / gather not applied yet (ga_flush)
     DevBuf recs, bnds, partials, plan, wpart, order, fctr;   // the generation's fused pipeline
+    DevBuf costs, blkmap;          // single-round packing: per-strip costs (breed) -> block map (launch_lpt)
+    // GGS_GA_LPT=1 at session creation: pack single-round rasters by strip cost.  Off:
+    // bit-identical, but measured slower at the shipped GA shape (the packing's
+    // kernel costs ~10 us, the raster gains < 1 %; docs/EXPERIMENTS.md §16)
+    bool lpt = false;
+    int lpt_head = LPT_HEAD, lpt_pk = LPT_PK, lpt_add = -1;   // cost model (GGS_LPT_HEAD/_PK/_ADD: experiments)
     int64_t n_curves = 0, curves_cap = 0;
     void* comm = nullptr;          // ggs_ga_set_comm: offspring fitness sharded over ranks
     int nranks = 1, rank = 0;
@@ -1125,29 +1210,6 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     const int onew = 1 - s->ocur;
     // per generation: breed (survivors + gather of the previous generation, then
     // variation + prep of the offspring), raster, finalize [, all-gather]
-    if (s->pending && ga_fused(s)) {
-        const int nxt = 1 - s->cur;
-        double* row;
-        if ((rc = ga_curves_row(s, &row))) return rc;
-        BreedDev br{(const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
-                    (const float*)s->off[s->ocur].p, (const float*)s->off_fits.p,
-                    (const int*)s->elite[s->cur].p, (int*)s->elite[nxt].p, (float*)s->pop[nxt].p,
-                    (float*)s->fits[nxt].p, row, ga_best(s), c.elite_k};
-        ProfScope ps(s->st, 0);
-        GGS_HIP(launch_ga_variation(s->st, nullptr, nullptr, P, N, prm, d, c.seed, gen, (float*)s->off[onew].p, P,
-                                    (SplatRec*)s->recs.p, (int4*)s->bnds.p, c.H, c.W, c.k_sigma, nullptr, nullptr,
-                                    &br));
-        s->cur = nxt;
-        s->n_curves += 1;
-    } else {
-        if ((rc = ga_flush(s))) return rc;
-        ProfScope ps(s->st, 0);
-        GGS_HIP(launch_ga_variation(s->st, (const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
-                                    P, N, prm, d, c.seed, gen, (float*)s->off[onew].p, P, (SplatRec*)s->recs.p,
-                                    (int4*)s->bnds.p, c.H, c.W, c.k_sigma));
-    }
-    s->ocur = onew;
-    s->pending = true;
     // Only offspring[:P - E] survive (algorithm.py:140-141: the next generation is the
     // E elites + the first P - E offspring, fitnesses likewise); the last E offspring's
     // fitness is never read (survivors, fused breed, best, curves), so they are bred
@@ -1157,11 +1219,57 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     // every rank bred all P offspring above with the same draws
     const int per = (Pe + s->nranks - 1) / s->nranks;
     const int b0 = std::min(Pe, s->rank * per), nb = std::min(Pe, b0 + per) - b0;
-    if (nb > 0 && (rc = raster_fitness(s->st, (const SplatRec*)s->recs.p + (int64_t)b0 * N,
+    const int G = raster_tiles(c.H, c.W, nullptr) * 4;
+    bool lpt = false;
+    if (s->pending && ga_fused(s)) {
+        const int nxt = 1 - s->cur;
+        double* row;
+        if ((rc = ga_curves_row(s, &row))) return rc;
+        BreedDev br{(const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
+                    (const float*)s->off[s->ocur].p, (const float*)s->off_fits.p,
+                    (const int*)s->elite[s->cur].p, (int*)s->elite[nxt].p, (float*)s->pop[nxt].p,
+                    (float*)s->fits[nxt].p, row, ga_best(s), c.elite_k};
+        // a single-round raster launch (2-3 strip-waves per SIMD): the breed writes the
+        // evaluated offspring's strip costs and launch_lpt packs them per SIMD
+        lpt = s->lpt && nb > 0 && lpt_applies(nb * G, s->c->simds, c.H, c.W);
+        if (lpt) {
+            if ((rc = ensure(s->costs, sizeof(int) * (size_t)nb * G, s->st)) ||
+                (rc = ensure(s->blkmap, sizeof(int) * (size_t)nb * G, s->st)))
+                return rc;
+            br.costs = (int*)s->costs.p;
+            br.cost_o0 = b0;
+            br.cost_n = nb;
+            br.cost_head = s->lpt_head;
+            br.cost_pk = s->lpt_pk;
+        }
+        {
+            ProfScope ps(s->st, 0);
+            GGS_HIP(launch_ga_variation(s->st, nullptr, nullptr, P, N, prm, d, c.seed, gen, (float*)s->off[onew].p,
+                                        P, (SplatRec*)s->recs.p, (int4*)s->bnds.p, c.H, c.W, c.k_sigma, nullptr,
+                                        nullptr, &br));
+        }
+        s->cur = nxt;
+        s->n_curves += 1;
+        if (lpt) {
+            ProfScope pl(s->st, 3);
+            GGS_HIP(launch_lpt(s->st, (const int*)s->costs.p, nb * G, s->c->simds,
+                               s->lpt_add >= 0 ? s->lpt_add : lpt_cost_add(N), (int*)s->blkmap.p));
+        }
+    } else {
+        if ((rc = ga_flush(s))) return rc;
+        ProfScope ps(s->st, 0);
+        GGS_HIP(launch_ga_variation(s->st, (const float*)s->pop[s->cur].p, (const float*)s->fits[s->cur].p,
+                                    P, N, prm, d, c.seed, gen, (float*)s->off[onew].p, P, (SplatRec*)s->recs.p,
+                                    (int4*)s->bnds.p, c.H, c.W, c.k_sigma));
+    }
+    s->ocur = onew;
+    s->pending = true;
+    if (nb > 0 && (rc = raster_fitness(s->st, s->c->simds, (const SplatRec*)s->recs.p + (int64_t)b0 * N,
                                        (const int4*)s->bnds.p + (int64_t)b0 * N, nb, N, c.H, c.W,
                                        (const float4*)s->plan.p, (float*)s->partials.p, (const float*)s->wpart.p,
                                        c.fitness_mode, (const int*)s->order.p, s->fctr,
-                                       (float*)s->off_fits.p + b0, true)))
+                                       (float*)s->off_fits.p + b0, true, nullptr, nullptr,
+                                       lpt ? (const int*)s->blkmap.p : nullptr)))
         return rc;
     if (s->comm && per > 0) {   // one in-place all-gather of the shards' fitness scalars (RCCL, same stream)
         float* of = (float*)s->off_fits.p;
@@ -1224,7 +1332,7 @@ int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, int4* bnds, flo
     if (dirty)
         GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, G, (const SplatRec*)s->cur_recs.p, recs, n,
                              s->N, c.H, c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p));
-    return raster_fitness(s->st, recs, bnds, n, s->N, c.H, c.W, (const float4*)s->plan.p, part,
+    return raster_fitness(s->st, s->c->simds, recs, bnds, n, s->N, c.H, c.W, (const float4*)s->plan.p, part,
                           (const float*)s->wpart.p, c.fitness_mode, (const int*)s->order.p, s->fctr, fits, false,
                           dirty ? (const unsigned char*)s->dirty.p : nullptr, (const float*)s->cur_part.p);
 }
@@ -1255,7 +1363,7 @@ void ga_free(GaSession* s) {
                       &s->src, &s->elite[0], &s->elite[1],
                       &s->target, &s->mask, &s->best_ind, &s->best_fit, &s->best_src, &s->best_upd,
                       &s->curves, &s->draws, &s->recs, &s->bnds, &s->partials, &s->plan, &s->wpart, &s->order,
-                      &s->fctr})
+                      &s->fctr, &s->costs, &s->blkmap})
         if (b->p) (void)hipFree(b->p);
     if (s->st) (void)hipStreamDestroy(s->st);
 }
@@ -1279,6 +1387,10 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     ga_fill_log_bounds(&s->cfg);
     s->P = c.pop_size;
     s->N = c.n_splats;
+    if (const char* v = getenv("GGS_GA_LPT")) s->lpt = atoi(v) != 0;
+    if (const char* v = getenv("GGS_LPT_HEAD")) s->lpt_head = atoi(v);
+    if (const char* v = getenv("GGS_LPT_PK")) s->lpt_pk = atoi(v);
+    if (const char* v = getenv("GGS_LPT_ADD")) s->lpt_add = atoi(v);
     const size_t pb = sizeof(float) * 9 * (size_t)s->P * s->N, hw = (size_t)c.H * c.W;
     // what every rank of a sharded session must agree on (ggs_ga_set_comm checks it)
     s->fingerprint = hash_bytes(&s->cfg, sizeof s->cfg) * 0x9E3779B97F4A7C15ull ^
@@ -1682,7 +1794,7 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
                                   c.H, c.W, bg, nullptr,
                                   (const float4*)s->plan.p, (float*)s->nb_part.p, (const int*)s->order.p,
                                   s->incremental ? (const unsigned char*)s->dirty.p : nullptr,
-                                  (const float*)s->cur_part.p, live));
+                                  (const float*)s->cur_part.p, live, nullptr, s->c->simds));
         }
         rd.gcap = bw;
         GGS_HIP(launch_sa_accept(s->st, loop, sit, rd));

@@ -7,10 +7,15 @@
 // The gather is enqueued by the library on the caller's stream (in order after
 // the fitness kernels) or on the communicator's own stream (overlap: the next
 // batch's raster runs while the scalars move).  RCCL is loaded at first use:
-// the copy already in the process when there is one (PyTorch bundles its own,
-// SONAME librccl.so.1, and ggs/_lib.py preloads it like the HIP runtime), else
-// $GGS_RCCL, else librccl.so.1 from the rpath (/opt/rocm/lib).
+// the copy already in the process when there is one (ggs/_lib.py preload_rccl
+// loads the one beside the HIP runtime, RTLD_LOCAL), else $GGS_RCCL, else
+// librccl.so.1 / librccl.so from the directory of the HIP runtime libggs is
+// bound to (by absolute path, never a search).  It must come from that same
+// directory (one ROCm tree: /opt/rocm's, or PyTorch's bundled copies): a mixed
+// pair is refused, because HIP and RCCL of different ROCm releases in one
+// process fail at the first N > 1 communicator (docs/EXPERIMENTS.md §16).
 #include <dlfcn.h>
+#include <limits.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>   // types and enums only; entry points are resolved by dlsym
 #include <stdarg.h>
@@ -42,6 +47,10 @@ int cfail(int code, const char* fmt, ...) {
 }
 
 struct Rccl {
+    ncclResult_t (*get_version)(int*) = nullptr;
+    ncclResult_t (*comm_count)(ncclComm_t, int*) = nullptr;
+    ncclResult_t (*comm_user_rank)(ncclComm_t, int*) = nullptr;
+    ncclResult_t (*comm_cu_device)(ncclComm_t, int*) = nullptr;
     ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
@@ -51,19 +60,41 @@ struct Rccl {
     ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
     std::string err;
+    std::string path;                    // the loaded library (realpath), "" before / on failure
+    int version = 0;
     bool ok = false;
 };
+
+// realpath of the shared object holding `sym` ("" if unknown)
+std::string object_path(const void* sym) {
+    Dl_info info{};
+    if (!sym || !dladdr(sym, &info) || !info.dli_fname) return "";
+    char buf[PATH_MAX];
+    return realpath(info.dli_fname, buf) ? std::string(buf) : std::string(info.dli_fname);
+}
+std::string dir_of(const std::string& p) {
+    const size_t k = p.rfind('/');
+    return k == std::string::npos ? std::string(".") : p.substr(0, k);
+}
+// the HIP runtime libggs is bound to
+std::string hip_runtime_path() { return object_path(reinterpret_cast<const void*>(&hipGetDevice)); }
 
 const Rccl& rccl() {
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
+        const std::string hip = hip_runtime_path(), hdir = dir_of(hip);
+        // RTLD_LOCAL: RCCL's exported libstdc++ template instantiations must not
+        // enter the global scope (PyTorch's bundled librccl, loaded RTLD_GLOBAL
+        // before torch, had torch's libraries bind their std::map / shared_ptr
+        // code to its copies: "double free or corruption" at exit, EXP §16)
         void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-        if (!h && getenv("GGS_RCCL")) h = dlopen(getenv("GGS_RCCL"), RTLD_NOW | RTLD_GLOBAL);
-        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h && getenv("GGS_RCCL")) h = dlopen(getenv("GGS_RCCL"), RTLD_NOW | RTLD_LOCAL);
+        for (const char* name : {"/librccl.so.1", "/librccl.so"})
+            if (!h && !hip.empty()) h = dlopen((hdir + name).c_str(), RTLD_NOW | RTLD_LOCAL);
         if (!h) {
             const char* e = dlerror();
-            r.err = std::string("cannot load RCCL (librccl.so.1): ") + (e ? e : "?");
+            r.err = std::string("cannot load RCCL beside the HIP runtime (") + hdir + "): " + (e ? e : "?");
             return;
         }
         r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
@@ -74,11 +105,28 @@ const Rccl& rccl() {
         r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
         r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
         r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+        r.get_version = (decltype(r.get_version))dlsym(h, "ncclGetVersion");
+        r.comm_count = (decltype(r.comm_count))dlsym(h, "ncclCommCount");
+        r.comm_user_rank = (decltype(r.comm_user_rank))dlsym(h, "ncclCommUserRank");
+        r.comm_cu_device = (decltype(r.comm_cu_device))dlsym(h, "ncclCommCuDevice");
         r.ok = r.get_unique_id && r.comm_init_rank && r.all_gather && r.comm_destroy && r.error_string &&
-               r.comm_init_all && r.group_start && r.group_end;
-        if (!r.ok) r.err = "RCCL is missing an entry point (ncclGetUniqueId / ncclCommInitRank / "
-                           "ncclCommInitAll / ncclAllGather / ncclGroupStart / ncclGroupEnd / "
-                           "ncclCommDestroy / ncclGetErrorString)";
+               r.comm_init_all && r.group_start && r.group_end && r.get_version && r.comm_count &&
+               r.comm_user_rank && r.comm_cu_device;
+        if (!r.ok) {
+            r.err = "RCCL is missing an entry point (ncclGetUniqueId / ncclCommInitRank / ncclCommInitAll / "
+                    "ncclAllGather / ncclGroupStart / ncclGroupEnd / ncclCommDestroy / ncclGetErrorString / "
+                    "ncclGetVersion / ncclCommCount / ncclCommUserRank / ncclCommCuDevice)";
+            return;
+        }
+        r.path = object_path(reinterpret_cast<const void*>(r.get_unique_id));
+        if (r.get_version(&r.version) != ncclSuccess) r.version = 0;
+        // one ROCm tree: RCCL from the HIP runtime's directory
+        if (hip.empty() || dir_of(r.path) != hdir) {
+            r.ok = false;
+            r.err = "RCCL " + r.path + " is not from the HIP runtime's tree (" + (hip.empty() ? "?" : hip) +
+                    "): refusing a process that mixes ROCm trees (load RCCL beside the HIP runtime: "
+                    "ggs._lib.preload_rccl)";
+        }
     });
     return r;
 }
@@ -135,6 +183,7 @@ struct Loop {
     std::vector<float*> recv;
     std::vector<int64_t> count;
     std::vector<hipEvent_t> ev, done;
+    std::string broken;                  // set when an enqueue failed part-way: the group is unusable
     // host gathers
     int64_t hgen = 0;
     int harrived = 0;
@@ -192,9 +241,16 @@ struct DevScope {
     ~DevScope() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
+// d_recv on rank r's stream is defined only once EVERY rank has called for this
+// gather: the last caller enqueues all the copies (ranks must be stepped in
+// lockstep; include/ggs.h).  A HIP failure part-way through that enqueue leaves
+// some streams with copies and others without, so the group is poisoned: every
+// later call fails with the first error instead of pairing the wrong gathers.
 int loop_allgather(Comm* c, hipStream_t stream, const float* d_send, float* d_recv, int64_t count) {
     Loop& L = *c->loop;
     std::lock_guard<std::mutex> lk(L.mu);
+    if (!L.broken.empty())
+        return cfail(GGS_EHIP, "loopback group unusable after an earlier failure: %s", L.broken.c_str());
     const int r = c->rank;
     if (L.have[r])
         return cfail(GGS_EINVAL, "loopback all-gather %lld: rank %d called again before every rank called "
@@ -211,21 +267,30 @@ int loop_allgather(Comm* c, hipStream_t stream, const float* d_send, float* d_re
     L.count[r] = count;
     if (++L.arrived < L.n) return GGS_OK;
     const size_t bytes = sizeof(float) * (size_t)count;
-    for (int q = 0; q < L.n; ++q) {               // rank q's stream receives every shard
-        for (int p = 0; p < L.n; ++p) {
+    hipError_t e = hipSuccess;
+    const char* what = "";
+    for (int q = 0; q < L.n && e == hipSuccess; ++q) {               // rank q's stream receives every shard
+        for (int p = 0; p < L.n && e == hipSuccess; ++p) {
             float* dst = L.recv[q] + (int64_t)p * count;
-            if (p != q) GGS_HIPC(hipStreamWaitEvent(L.st[q], L.ev[p], 0));
-            if (bytes && dst != L.send[p])
-                GGS_HIPC(hipMemcpyAsync(dst, L.send[p], bytes, hipMemcpyDeviceToDevice, L.st[q]));
+            if (p != q && (e = hipStreamWaitEvent(L.st[q], L.ev[p], 0)) != hipSuccess) what = "hipStreamWaitEvent";
+            else if (bytes && dst != L.send[p] &&
+                     (e = hipMemcpyAsync(dst, L.send[p], bytes, hipMemcpyDeviceToDevice, L.st[q])) != hipSuccess)
+                what = "hipMemcpyAsync";
         }
-        GGS_HIPC(hipEventRecord(L.done[q], L.st[q]));
+        if (e == hipSuccess && (e = hipEventRecord(L.done[q], L.st[q])) != hipSuccess) what = "hipEventRecord";
     }
-    for (int q = 0; q < L.n; ++q)
-        for (int p = 0; p < L.n; ++p)
-            if (p != q) GGS_HIPC(hipStreamWaitEvent(L.st[q], L.done[p], 0));
+    for (int q = 0; q < L.n && e == hipSuccess; ++q)
+        for (int p = 0; p < L.n && e == hipSuccess; ++p)
+            if (p != q && (e = hipStreamWaitEvent(L.st[q], L.done[p], 0)) != hipSuccess) what = "hipStreamWaitEvent";
     std::fill(L.have.begin(), L.have.end(), 0);
     L.arrived = 0;
     ++L.seq;
+    if (e != hipSuccess) {
+        char m[256];
+        snprintf(m, sizeof m, "gather %lld: %s: %s", (long long)(L.seq - 1), what, hipGetErrorString(e));
+        L.broken = m;
+        return cfail(GGS_EHIP, "loopback all-gather failed part-way (%s); the group is now unusable", m);
+    }
     return GGS_OK;
 }
 
@@ -355,6 +420,52 @@ int ggs_comm_wait(void* comm, void* stream, int64_t ticket) {
     DevScope ds(c->dev);
     // a slot reused by a later ticket still orders after `ticket` (one side stream)
     GGS_HIPC(hipStreamWaitEvent((hipStream_t)stream, c->done[ticket % kTickets], 0));
+    return GGS_OK;
+}
+
+int ggs_comm_info(void* comm, int32_t* nranks, int32_t* rank, int32_t* device) {
+    Comm* c = (Comm*)comm;
+    if (!c) return cfail(GGS_EINVAL, "ggs_comm_info: no communicator");
+    if (c->loop || !c->nc) return cfail(GGS_EINVAL, "ggs_comm_info: not an RCCL communicator (loopback group)");
+    const Rccl& R = rccl();
+    if (!R.ok) return cfail(GGS_ENODEV, "%s", R.err.c_str());
+    int n = 0, r = 0, d = 0;
+    GGS_NCCL(R.comm_count(c->nc, &n));
+    GGS_NCCL(R.comm_user_rank(c->nc, &r));
+    GGS_NCCL(R.comm_cu_device(c->nc, &d));
+    if (nranks) *nranks = n;
+    if (rank) *rank = r;
+    if (device) *device = d;
+    return GGS_OK;
+}
+
+int ggs_runtime_info(char* buf, int32_t cap) {
+    // RCCL as loaded by this library (not loaded by this call: null until a
+    // communicator or ggs_comm_unique_id needed it)
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    const std::string hip = hip_runtime_path();
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    std::string rpath;
+    int ver = 0;
+    if (h) {
+        void* f = dlsym(h, "ncclGetUniqueId");
+        rpath = object_path(f);
+        auto gv = (ncclResult_t(*)(int*))dlsym(h, "ncclGetVersion");
+        if (!gv || gv(&ver) != ncclSuccess) ver = 0;
+        dlclose(h);
+    }
+    int hv = 0;
+    if (hipRuntimeGetVersion(&hv) != hipSuccess) hv = 0;
+    auto q = [](const std::string& x) { return x.empty() ? std::string("null") : "\"" + x + "\""; };
+    std::string j = "{\"hip\": " + q(hip) + ", \"hip_version\": " + std::to_string(hv) + ", \"rccl\": " + q(rpath) +
+                    ", \"rccl_version\": " + (rpath.empty() ? std::string("null") : std::to_string(ver)) +
+                    ", \"same_tree\": " +
+                    (rpath.empty() || hip.empty() ? std::string("null")
+                                                  : std::string(dir_of(rpath) == dir_of(hip) ? "true" : "false")) +
+                    "}";
+    if (!buf || cap <= (int32_t)j.size()) return (int32_t)j.size() + 1;     // the size needed
+    memcpy(buf, j.c_str(), j.size() + 1);
     return GGS_OK;
 }
 

@@ -61,6 +61,7 @@ SIGNATURES = {
                                      C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_float,
                                      C.c_int32, C.c_int32, C.c_float, C.c_void_p]),
     "ggs_detmath_eval": (C.c_int, [C.c_int32, _f32p, _f32p, C.c_int64, _f32p]),
+    "ggs_lpt_pack": (C.c_int, [_i32p, C.c_int32, C.c_int32, C.c_int32, _i32p]),
     "ggs_profile_enable": (C.c_int, [C.c_int32]),
     "ggs_profile_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "ggs_profile_reset": (None, []),
@@ -98,6 +99,8 @@ SIGNATURES = {
                                      C.c_int32, C.POINTER(C.c_int64)]),
     "ggs_comm_wait": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
     "ggs_comm_size": (C.c_int, [C.c_void_p, _i32p, _i32p]),
+    "ggs_comm_info": (C.c_int, [C.c_void_p, _i32p, _i32p, _i32p]),
+    "ggs_runtime_info": (C.c_int, [C.c_char_p, C.c_int32]),
     "ggs_comm_destroy": (None, [C.c_void_p]),
     "ggs_ga_set_comm": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ggs_comm_init_local": (C.c_int, [C.c_int32, _i32p, C.POINTER(C.c_void_p)]),
@@ -121,61 +124,93 @@ class GGSInputError(AssertionError, ValueError):
     (render.py:219, :223), hence the AssertionError base; ValueError too."""
 
 
-def _share_hip_runtime_with_torch() -> None:
-    """One HIP runtime per process.  PyTorch-ROCm wheels bundle their own
-    libamdhip64 (same SONAME as /opt/rocm's).  If libggs binds /opt/rocm's copy
-    first, a later ``import torch`` loads a second runtime and whichever
-    initialises second finds no GPU.  The reference's callers hand us torch
-    tensors, so when torch is installed (not necessarily imported) its runtime is
-    loaded first (RTLD_GLOBAL) and libggs binds to it by SONAME.
-    GGS_HIP_RUNTIME=system skips this."""
-    if os.environ.get("GGS_HIP_RUNTIME", "") == "system":
-        return
+def _torch_lib_dir():
     import importlib.util
     try:
         spec = importlib.util.find_spec("torch")
     except (ImportError, ValueError):
-        return
+        return None
     if spec is None or not spec.submodule_search_locations:
-        return
-    tlib = os.path.join(list(spec.submodule_search_locations)[0], "lib")
-    hip = os.path.join(tlib, "libamdhip64.so")
-    if os.path.exists(hip):
-        for dep in ("libhsa-runtime64.so", "libamdhip64.so"):
-            p = os.path.join(tlib, dep)
-            if os.path.exists(p):
-                C.CDLL(p, mode=C.RTLD_GLOBAL)
+        return None
+    d = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    return d if os.path.exists(os.path.join(d, "libamdhip64.so")) else None
+
+
+def rocm_lib_dir() -> str:
+    """/opt/rocm's library directory ($ROCM_PATH), resolved to its release tree."""
+    return os.path.realpath(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib"))
+
+
+# the runtime libraries this module loaded by absolute path (kept referenced)
+_runtime_handles = []
+
+
+def _bind_hip_runtime() -> None:
+    """One HIP runtime per process, loaded by absolute path before libggs (which
+    binds it by SONAME, libamdhip64.so.7, so it takes the one already loaded).
+    PyTorch-ROCm wheels bundle their own libamdhip64 under the same SONAME: if
+    libggs bound /opt/rocm's copy first, a later ``import torch`` would load a
+    second runtime and whichever initialises second finds no GPU.  The
+    reference's callers hand us torch tensors, so when torch is installed (not
+    necessarily imported) its runtime is the one.  GGS_HIP_RUNTIME=system:
+    $ROCM_PATH's (/opt/rocm), by absolute path — a bare SONAME search can resolve
+    to torch's copy through the library path (the round-5 bench line ran on it)."""
+    if os.environ.get("GGS_HIP_RUNTIME", "") == "system":
+        d = rocm_lib_dir()
+        names = ("libhsa-runtime64.so.1", "libamdhip64.so.7")
+    else:
+        d = _torch_lib_dir()
+        names = ("libhsa-runtime64.so", "libamdhip64.so")
+        if d is None:
+            return                      # no torch: libggs's own runpath (/opt/rocm/lib)
+    for n in names:
+        p = os.path.join(d, n)
+        if not os.path.exists(p):
+            raise ImportError(f"HIP runtime {p} not found (GGS_HIP_RUNTIME="
+                              f"{os.environ.get('GGS_HIP_RUNTIME', '')!r}, ROCM_PATH)")
+        _runtime_handles.append(C.CDLL(p, mode=C.RTLD_GLOBAL))
+
+
+def mapped(name: str):
+    """Paths of this process's mapped shared objects whose file name starts with `name`."""
+    out = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1]
+                if os.path.basename(p).startswith(name) and p not in out:
+                    out.append(p)
+    except OSError:
+        pass
+    return out
 
 
 def preload_rccl() -> None:
-    """Same rule for RCCL (ggs_comm_*): PyTorch bundles its own librccl with the
-    SONAME of /opt/rocm's, so libggs's dlopen must find the copy torch.distributed
-    uses.  Called before the first communicator is made.  torch itself is imported
-    here, not just its librccl: a process that initialised RCCL and imported torch
-    only afterwards aborted at interpreter exit ("double free or corruption", after
-    every call had returned; tools/probe/exit_bisect.sh: tests/test_gpu_comm.py then
-    test_gpu_parity.py's torch tests), while torch imported first never did."""
-    if os.environ.get("GGS_HIP_RUNTIME", "") == "system":
-        return
-    import importlib.util
-    try:
-        spec = importlib.util.find_spec("torch")
-    except (ImportError, ValueError):
-        return
-    if spec is None or not spec.submodule_search_locations:
-        return
-    try:
-        import torch  # noqa: F401  (loads its librccl as well)
-        return
-    except Exception:  # noqa: BLE001 — a broken torch install: bind its librccl only
-        pass
-    p = os.path.join(list(spec.submodule_search_locations)[0], "lib", "librccl.so")
-    if os.path.exists(p):
-        C.CDLL(p, mode=C.RTLD_GLOBAL)
+    """Load the RCCL of the HIP runtime's tree (its directory: /opt/rocm's or
+    PyTorch's bundled one, which torch.distributed uses) by absolute path,
+    RTLD_LOCAL, before the first communicator; libggs finds it by SONAME and
+    refuses an RCCL from another directory.  RTLD_LOCAL is the fix for the exit
+    abort of round 5 (docs/EXPERIMENTS.md §16): PyTorch's librccl exports 223 weak
+    libstdc++ template instantiations (std::_Rb_tree<std::string, ...>::_M_erase,
+    shared_ptr's _M_release_last_use_cold, ...); loaded RTLD_GLOBAL before
+    ``import torch``, the torch libraries loaded later bound those calls to its
+    copies (LD_DEBUG=bindings: libtorch_cpu, libtorch_python, libc10, librocfft,
+    libhipblaslt, MIOpen, ...) and the interpreter aborted at exit with "double free
+    or corruption" — reproduced on a CPU host with no GPU, gone with RTLD_LOCAL."""
+    hips = mapped("libamdhip64")
+    if len(hips) != 1:
+        raise ImportError(f"expected one HIP runtime in the process, found {hips}")
+    d = os.path.dirname(os.path.realpath(hips[0]))
+    for n in ("librccl.so.1", "librccl.so"):
+        p = os.path.join(d, n)
+        if os.path.exists(p):
+            _runtime_handles.append(C.CDLL(p, mode=C.RTLD_LOCAL))
+            return
+    # none beside it: libggs reports the failure at the first communicator
 
 
 def _load() -> C.CDLL:
-    _share_hip_runtime_with_torch()
+    _bind_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libggs.so not found at {LIB_PATH}: build it with "
@@ -251,3 +286,15 @@ def ensure_init() -> int:
         if rc < 0:
             check(rc, "ggs_init")
         return rc
+
+
+def runtime_info() -> dict:
+    """ggs_runtime_info: the HIP runtime libggs is bound to and the RCCL it loaded
+    (paths, versions, one tree or not) — what a run's record names."""
+    import json
+    need = lib.ggs_runtime_info(None, 0)
+    buf = C.create_string_buffer(max(int(need), 1))
+    rc = lib.ggs_runtime_info(buf, len(buf))
+    if rc != GGS_OK:
+        raise GGSError(f"ggs_runtime_info: {rc}")
+    return json.loads(buf.value.decode())

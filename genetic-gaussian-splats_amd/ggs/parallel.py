@@ -290,6 +290,14 @@ class RcclGather:
     def barrier(self) -> None:
         self._lib.check(self._lib.lib.ggs_comm_barrier(self.handle), "ggs_comm_barrier")
 
+    def info(self):
+        """(ranks, rank, device) as RCCL itself reports them (ncclCommCount,
+        ncclCommUserRank, ncclCommCuDevice) — not the values this object was asked for."""
+        n, r, d = self._C.c_int32(0), self._C.c_int32(0), self._C.c_int32(0)
+        self._lib.check(self._lib.lib.ggs_comm_info(self.handle, self._C.byref(n), self._C.byref(r),
+                                                    self._C.byref(d)), "ggs_comm_info")
+        return n.value, r.value, d.value
+
     def close(self) -> None:
         if self.handle:
             self._lib.lib.ggs_comm_destroy(self.handle)
@@ -307,7 +315,10 @@ def loopback_group(device: int, n: int) -> list:
     job (``ggs_comm_init_loopback``; a test rig, no RCCL): the sharded code paths
     (rank != 0, uneven and empty shards, the GA's fingerprint exchange) run on a
     one-GPU box.  Device all-gathers must be issued in lockstep (every rank once
-    per gather); host all-gathers need one host thread per rank.  Each returned
+    per gather): the last rank's call enqueues every shard copy, so a rank's
+    d_recv is defined on its stream only after all ranks have called for that
+    gather; a HIP failure during that enqueue makes the group unusable (every later
+    call fails).  Host all-gathers need one host thread per rank.  Each returned
     object has RcclGather's interface."""
     from . import _lib
     arr = (C.c_void_p * int(n))()

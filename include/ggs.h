@@ -103,6 +103,15 @@ int ggs_preprocess(const float* genomes, int64_t S, int32_t C, int32_t H, int32_
  * 4 sqrt (correctly rounded), 5 x[i] / y[i] (correctly rounded). */
 int ggs_detmath_eval(int32_t fn, const float* x, const float* y, int64_t n, float* out);
 
+/* Single-round packing (the device GA's raster launch of n strip-waves with
+ * 2*simds < n <= 3*simds, at most 4,096): costs[i] (+ cost_add) of strip i ->
+ * map[r + k*simds] = the strip block r + k*simds runs, a permutation of [0, n)
+ * that packs three strips per SIMD (blocks r, r + simds, r + 2*simds share SIMD
+ * r), largest first in rounds.  Order only (the raster's bits never depend on
+ * it).  Runs the device kernel the GA uses; replaces the centre-first grid order
+ * of render.py:240-251's single launch for these shapes. */
+int ggs_lpt_pack(const int32_t* costs, int32_t n, int32_t simds, int32_t cost_add, int32_t* map);
+
 /* ---- device-pointer API (inputs resident in HBM) ----------------------------
  * Same semantics as the host API on one device; all pointers are device
  * pointers on `device`; work is enqueued on `stream` (a hipStream_t, NULL =
@@ -247,8 +256,9 @@ void ggs_sa_destroy(void* handle);
  * exchange is an all-gather of each rank's fitness scalars over RCCL (xGMI).
  * Replaces nothing in the reference (single-device, render.py:4); it is the
  * collective of the sharded fitness_population (fitness.py:34-47).  RCCL is
- * loaded at first use (the copy already in the process, else $GGS_RCCL, else
- * librccl.so.1).  Rank 0 makes the id, every rank passes the same bytes. */
+ * loaded at first use (the copy already in the process, else $GGS_RCCL, else the
+ * one beside the HIP runtime, by absolute path) and must come from the HIP
+ * runtime's directory.  Rank 0 makes the id, every rank passes the same bytes. */
 #define GGS_COMM_ID_BYTES 128
 int ggs_comm_unique_id(uint8_t* id128);
 int ggs_comm_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* id128, void** comm);
@@ -263,6 +273,16 @@ int ggs_comm_allgather(void* comm, void* stream, const float* d_send, float* d_r
  * valid for the 64 most recent tickets. */
 int ggs_comm_wait(void* comm, void* stream, int64_t ticket);
 int ggs_comm_size(void* comm, int32_t* nranks, int32_t* rank);
+/* What RCCL itself reports for `comm` (ncclCommCount, ncclCommUserRank,
+ * ncclCommCuDevice); GGS_EINVAL for a loopback communicator (no RCCL). */
+int ggs_comm_info(void* comm, int32_t* nranks, int32_t* rank, int32_t* device);
+/* Provenance of the runtimes in this process, as JSON into buf[cap]: the HIP
+ * runtime libggs is bound to (path, version), the RCCL libggs loaded (path,
+ * version; null before the first communicator) and whether both come from one
+ * directory.  RCCL is always loaded from the HIP runtime's directory and a mixed
+ * pair is refused (ggs_comm_* fail with GGS_ENODEV).  Returns 0, or the buffer
+ * size needed (> 0) when cap is too small. */
+int ggs_runtime_info(char* buf, int32_t cap);
 void ggs_comm_destroy(void* comm);
 /* Single-process communicators over the n listed devices (ncclCommInitAll; no id
  * exchange): comms[i] is rank i on devices[i].  The host API uses this for its
@@ -273,7 +293,10 @@ int ggs_comm_init_local(int32_t n, const int32_t* devices, void** comms);
  * paths (rank != 0, uneven and empty shards, ggs_ga_set_comm's fingerprint
  * check).  Device all-gathers are matched by call order: every rank calls once
  * per gather (lockstep; a second call before all ranks called fails), the last
- * call enqueues the shard copies on every rank's stream.  Host all-gathers /
+ * call enqueues the shard copies on every rank's stream — so d_recv on rank r's
+ * stream is defined only after EVERY rank has called for that gather (work a
+ * rank queues on its stream before then does not see it).  A HIP failure while
+ * the last call enqueues poisons the group (every later call fails).  Host all-gathers /
  * barriers block until all n ranks (on their own host threads) arrived, at most
  * GGS_LOOPBACK_TIMEOUT_S seconds (default 60), then fail. */
 int ggs_comm_init_loopback(int32_t device, int32_t n, void** comms);
@@ -285,7 +308,7 @@ int ggs_comm_allgather_host(void* comm, const float* send, float* recv, int64_t 
 int ggs_comm_barrier(void* comm);
 
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------
- * When enabled, every launch of "prep", "raster" and "finalize" is bracketed
+ * When enabled, every launch of "prep", "raster", "finalize" and "lpt" is bracketed
  * by hipEvents; ggs_profile_read synchronises those events and returns the
  * accumulated milliseconds and launch count for the named kernel (a finalize
  * folded into the raster counts as raster time, no finalize launch). */

@@ -159,6 +159,10 @@ class PipeComm:
     def barrier(self):
         self._exchange("barrier", np.zeros(0, np.float32))
 
+    def info(self):
+        """(ranks, rank, device) as RCCL reports them: this rank's device is its LOCAL_RANK."""
+        return self.world, self.rank, int(self.log.get("device", -1)) if self.log is not None else -1
+
     def close(self):
         pass
 
@@ -240,6 +244,8 @@ def install_fake_gpu(mesh, rank, world, log, slow_rank=None, corrupt=False, stal
     ggs.profile_enable = lambda on: None
     ggs.profile_read = lambda k: (0.1, 1)
     ggs.encode = lambda G: np.asarray(G, np.float32)
+    ggs.runtime_info = lambda: {"hip": "/fake/rocm/lib/libamdhip64.so.7", "hip_version": 1,
+                                "rccl": "/fake/rocm/lib/librccl.so.1", "rccl_version": 1, "same_tree": True}
 
     def preprocess(G, H, W, k):
         n = int(np.prod(G.shape[:-1]))

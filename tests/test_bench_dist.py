@@ -108,6 +108,9 @@ def test_bench_world_n_orchestration(tmp_path, world):
     line = json.loads(out0[0])
     assert line["n_gpus"] == world and line["config"]["global_batch"] == 128 * world
     assert line["config"]["rccl_ranks"] == world and len(out0) == 1
+    # rank -> device from each rank's communicator (RCCL's own report), gathered
+    assert line["config"]["rank_devices"] == [[r, r] for r in range(world)]
+    assert line["runtime"]["same_tree"] is True
 
 
 def test_bench_world2_strong_scaling_splits_configs3(tmp_path):

@@ -50,6 +50,53 @@ def test_rccl_allgather_returns_every_shard(hip, overlap, monkeypatch):
         comm.close()
 
 
+def test_rccl_reports_world1_and_one_tree(hip):
+    """The rank count a run reports is RCCL's own (ncclCommCount /
+    ncclCommUserRank / ncclCommCuDevice), and HIP + RCCL come from one directory."""
+    comm = ggs.RcclGather(0, rank=0, world=1)
+    try:
+        assert comm.info() == (1, 0, 0)
+        info = ggs.runtime_info()
+        assert info["same_tree"] is True, info
+        assert os.path.dirname(info["rccl"]) == os.path.dirname(info["hip"])
+        assert info["rccl_version"] > 0 and info["hip_version"] > 0
+        from ggs import _lib
+        assert len(_lib.mapped("libamdhip64")) == 1 and len(_lib.mapped("librccl")) == 1
+    finally:
+        comm.close()
+    lb = ggs.parallel.loopback_group(0, 2)
+    with pytest.raises(ggs.GGSInputError):            # no RCCL behind a loopback rank
+        lb[0].info()
+    for g in lb:
+        g.close()
+
+
+_COMM_THEN_TORCH = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import ggs
+from ggs import hip
+comm = ggs.RcclGather(0, rank=0, world=1)
+st = hip.Stream()
+x = hip.DeviceArray.from_host(np.arange(64, dtype=np.float32))
+y = hip.DeviceArray((64,))
+comm.allgather(st.handle, x.ptr, y.ptr, 64)
+assert (y.to_host(st) == np.arange(64)).all()
+comm.close()
+import torch
+print("ok", torch.__version__)
+"""
+
+
+def test_comm_then_torch_exits_cleanly():
+    """Round 5's exit abort (a communicator made, torch imported afterwards):
+    status 0 and no allocator error now that RCCL is loaded RTLD_LOCAL."""
+    r = subprocess.run([sys.executable, "-c", _COMM_THEN_TORCH, PKG], capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, GGS_COMM_RCCL_SELF="1"))
+    assert r.returncode == 0 and "ok" in r.stdout, (r.returncode, r.stderr[-2000:])
+    assert "double free" not in r.stderr and "free()" not in r.stderr
+
+
 def test_host_allgather_and_barrier(hip):
     comm = ggs.RcclGather(0, rank=0, world=1)
     try:

@@ -43,6 +43,7 @@ def _problem(H, W, seed):
     (64, 64, 32, 512, 3, 2, 8, 0.05, 0.05, False, 6),  # config.py's shape: N 512, pop 32, elite 8
     (40, 40, 12, 700, 2, 2, 2, 0.5, 0.1, False, 7),    # 512 < N <= 1024: 1024-thread workgroups
     (32, 40, 10, 1100, 2, 2, 2, 0.5, 0.1, True, 8),    # N > 1024: generic multi-pass workgroup loops
+    (24, 24, 64, 1100, 2, 2, 4, 0.5, 0.1, False, 9),   # N > 1024, P >= 64: 256-thread generic breed
     (32, 32, 8, 2, 5, 2, 1, 0.3, 0.01, False, 3),      # N = 2, rare mutation -> fallbacks
     (24, 24, 6, 1, 3, 2, 0, 0.5, 0.5, False, 4),       # N = 1: no swap; elite_k 0 -> 1
     (16, 16, 600, 3, 2, 3, 25, 0.5, 0.1, False, 5),    # P > 512: bitonic survivors path
@@ -154,37 +155,49 @@ init = ga.new_population(P, N, H, W, 3.0, 0.1, np.random.default_rng(0))
 cfg = dict(mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0, "alpha": 25.0},
            mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0, "alpha": 2.0},
            schedule="cosine")
+import ggs
+ggs.profile_enable(True)
 dga = DeviceGA(t, m, init, tour_k=2, elite_k=8, cxpb=0.05, mutpb=0.05, min_scale_splats=3.0,
                max_scale_splats=0.1, seed=1, **cfg)
 dga.run(1, 25, 25)
 st = dga.read()
 np.savez(sys.argv[2], population=st["population"], fitness=st["fitness"], best=st["best"],
-         best_fit=st["best_fit"], **{"c_" + k: np.asarray(v) for k, v in st["curves"].items()})
+         best_fit=st["best_fit"], **{"c_" + k: np.asarray(v) for k, v in st["curves"].items()},
+         lpt_launches=np.int64(ggs.profile_read("lpt")[1]))
 """
 
 
-@pytest.mark.parametrize("P,N", [(128, 256), (32, 512)])
+@pytest.mark.parametrize("P,N", [(128, 256), (32, 512), (32, 1100)])
 def test_device_ga_fused_breed_equals_unfused(tmp_path, P, N):
     """The fused breed (survivors + gather inside the variation kernel) against the
     five-launch generation (GGS_GA_UNFUSED=1), and the finalize folded into the
     raster against its own launch (GGS_UNFUSED_FINALIZE=1), at the bench workload
     and at the reference's shipped run (config.py: 512 splats, pop 32), 25
     generations of Philox draws in one run: identical populations, fitness, best
-    and curves."""
+    and curves.  At the shipped run (24 evaluated x 128 strips = one round on
+    MI355X's 1,024 SIMDs) GGS_GA_LPT=1 packs the raster by exact strip cost
+    (launch_lpt; off by default): the same bits either way."""
     import os
     import subprocess
     import sys
     pkg = os.path.dirname(os.path.dirname(ggs.__file__))
     out = {}
     for tag, env in (("fused", {}), ("unfused", {"GGS_GA_UNFUSED": "1"}),
-                     ("unfused_fin", {"GGS_UNFUSED_FINALIZE": "1"})):
+                     ("unfused_fin", {"GGS_UNFUSED_FINALIZE": "1"}), ("lpt", {"GGS_GA_LPT": "1"})):
         path = str(tmp_path / f"{tag}.npz")
         subprocess.run([sys.executable, "-c", _FUSED_SCRIPT, pkg, path, str(P), str(N)], check=True, timeout=300,
                        env=dict(os.environ, **env))
         out[tag] = np.load(path)
     for k in out["fused"].files:
+        if k == "lpt_launches":
+            continue
         np.testing.assert_array_equal(out["fused"][k], out["unfused"][k], err_msg=k)
         np.testing.assert_array_equal(out["fused"][k], out["unfused_fin"][k], err_msg=k)
+        np.testing.assert_array_equal(out["fused"][k], out["lpt"][k], err_msg=k)
+    assert int(out["fused"]["lpt_launches"]) == 0 and int(out["unfused"]["lpt_launches"]) == 0
+    if P == 32:      # one round of strip-waves on a 256-CU MI355X: packed every fused generation
+        # (N = 1100: the generic breed path, several splats per thread, writes the costs)
+        assert int(out["lpt"]["lpt_launches"]) == 24, int(out["lpt"]["lpt_launches"])
 
 
 def test_device_ga_sessions_concurrent_uneven_load_equal_solo():
