@@ -180,9 +180,9 @@ std::vector<int> g_active;                    // devices the host API fans out o
 bool g_inited = false;
 
 // ---- profiling ----------------------------------------------------------------
-constexpr int kProfKernels = 4;
+constexpr int kProfKernels = 3;
 struct ProfRec {
-    int kernel;  // 0 prep, 1 raster, 2 finalize, 3 lpt (single-round packing)
+    int kernel;  // 0 prep, 1 raster, 2 finalize
     hipEvent_t a, b;
 };
 std::mutex g_prof_mu;
@@ -190,7 +190,7 @@ bool g_prof_on = false;
 std::vector<ProfRec> g_prof_pending;
 double g_prof_ms[kProfKernels] = {};
 int64_t g_prof_n[kProfKernels] = {};
-const char* const kKernelNames[kProfKernels] = {"prep", "raster", "finalize", "lpt"};
+const char* const kKernelNames[kProfKernels] = {"prep", "raster", "finalize"};
 
 struct ProfScope {
     bool on = false;
@@ -232,7 +232,7 @@ void prof_drain_locked() {
 int raster_fitness(hipStream_t st, int simds, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                    const float4* plan, float* partials, const float* wpartials, int mode, const int* order,
                    DevBuf& ctr, float* out, bool fuse, const unsigned char* dirty = nullptr,
-                   const float* clean = nullptr, const int* blk_map = nullptr) {
+                   const float* clean = nullptr) {
     const float bg[3] = {1.f, 1.f, 1.f};  // fitness renders with the default background (fitness.py:15)
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
@@ -251,13 +251,13 @@ int raster_fitness(hipStream_t st, int simds, const SplatRec* recs, const int4* 
         ff.mode = mode;
         ProfScope ps(st, 1);
         GGS_HIP(launch_raster(st, 1, recs, bnds, B, N, H, W, bg, nullptr, plan, partials, order, dirty, clean,
-                              nullptr, &ff, simds, blk_map));
+                              nullptr, &ff, simds));
         return GGS_OK;
     }
     {
         ProfScope ps(st, 1);
         GGS_HIP(launch_raster(st, 1, recs, bnds, B, N, H, W, bg, nullptr, plan, partials, order, dirty, clean,
-                              nullptr, nullptr, simds, blk_map));
+                              nullptr, nullptr, simds));
     }
     ProfScope ps(st, 2);
     GGS_HIP(launch_finalize(st, partials, wpartials, B, nTiles, mode, H, W, out));
@@ -997,33 +997,6 @@ int ggs_detmath_eval(int32_t fn, const float* x, const float* y, int64_t n, floa
     return GGS_OK;
 }
 
-int ggs_lpt_pack(const int32_t* costs, int32_t n, int32_t simds, int32_t cost_add, int32_t* map) {
-    if (n < 0 || (n > 0 && (!costs || !map)) || simds < 1)
-        return fail(GGS_EINVAL, "ggs_lpt_pack: need n >= 0, costs, map and simds >= 1");
-    if (n > 0 && !(n > 2 * simds && n <= 3 * simds && n <= LPT_MAX))
-        return fail(GGS_EINVAL, "ggs_lpt_pack: n = %d strips is not one round of 2-3 waves on %d SIMDs (n <= %d)", n,
-                    simds, LPT_MAX);
-    if (n == 0) return GGS_OK;
-    int rc;
-    std::vector<DevCtx*> cs;
-    if ((rc = active_ctxs(1, &cs))) return rc;
-    DevCtx* c = cs[0];
-    std::lock_guard<std::mutex> lk(c->mu);
-    DeviceGuard dg(c->dev);
-    struct Scratch {
-        void* p = nullptr;
-        ~Scratch() { if (p) (void)hipFree(p); }
-    } dc, dm;
-    const size_t nb = sizeof(int) * (size_t)n;
-    GGS_HIP(hipMalloc(&dc.p, nb));
-    GGS_HIP(hipMalloc(&dm.p, nb));
-    GGS_HIP(hipMemcpy(dc.p, costs, nb, hipMemcpyHostToDevice));
-    GGS_HIP(launch_lpt(c->stream, (const int*)dc.p, n, simds, cost_add, (int*)dm.p));
-    GGS_HIP(hipStreamSynchronize(c->stream));
-    GGS_HIP(hipMemcpy(map, dm.p, nb, hipMemcpyDeviceToHost));
-    return GGS_OK;
-}
-
 int ggs_profile_enable(int32_t on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;
@@ -1040,7 +1013,7 @@ int ggs_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
             return GGS_OK;
         }
     }
-    return fail(GGS_EINVAL, "unknown kernel name '%s' (prep|raster|finalize|lpt)", kernel ? kernel : "(null)");
+    return fail(GGS_EINVAL, "unknown kernel name '%s' (prep|raster|finalize)", kernel ? kernel : "(null)");
 }
 
 void ggs_profile_reset(void) {
@@ -1077,12 +1050,6 @@ struct GaSession {
     int ocur = 0;                  // off[ocur]: the offspring evaluated last
     bool pending = false;          // their survivors / gather not applied yet (ga_flush)
     DevBuf recs, bnds, partials, plan, wpart, order, fctr;   // the generation's fused pipeline
-    DevBuf costs, blkmap;          // single-round packing: per-strip costs (breed) -> block map (launch_lpt)
-    // GGS_GA_LPT=1 at session creation: pack single-round rasters by strip cost.  Off:
-    // bit-identical, but measured slower at the shipped GA shape (the packing's
-    // kernel costs ~10 us, the raster gains < 1 %; docs/EXPERIMENTS.md §16)
-    bool lpt = false;
-    int lpt_head = LPT_HEAD, lpt_pk = LPT_PK, lpt_add = -1;   // cost model (GGS_LPT_HEAD/_PK/_ADD: experiments)
     int64_t n_curves = 0, curves_cap = 0;
     void* comm = nullptr;          // ggs_ga_set_comm: offspring fitness sharded over ranks
     int nranks = 1, rank = 0;
@@ -1219,8 +1186,6 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
     // every rank bred all P offspring above with the same draws
     const int per = (Pe + s->nranks - 1) / s->nranks;
     const int b0 = std::min(Pe, s->rank * per), nb = std::min(Pe, b0 + per) - b0;
-    const int G = raster_tiles(c.H, c.W, nullptr) * 4;
-    bool lpt = false;
     if (s->pending && ga_fused(s)) {
         const int nxt = 1 - s->cur;
         double* row;
@@ -1229,19 +1194,6 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
                     (const float*)s->off[s->ocur].p, (const float*)s->off_fits.p,
                     (const int*)s->elite[s->cur].p, (int*)s->elite[nxt].p, (float*)s->pop[nxt].p,
                     (float*)s->fits[nxt].p, row, ga_best(s), c.elite_k};
-        // a single-round raster launch (2-3 strip-waves per SIMD): the breed writes the
-        // evaluated offspring's strip costs and launch_lpt packs them per SIMD
-        lpt = s->lpt && nb > 0 && lpt_applies(nb * G, s->c->simds, c.H, c.W);
-        if (lpt) {
-            if ((rc = ensure(s->costs, sizeof(int) * (size_t)nb * G, s->st)) ||
-                (rc = ensure(s->blkmap, sizeof(int) * (size_t)nb * G, s->st)))
-                return rc;
-            br.costs = (int*)s->costs.p;
-            br.cost_o0 = b0;
-            br.cost_n = nb;
-            br.cost_head = s->lpt_head;
-            br.cost_pk = s->lpt_pk;
-        }
         {
             ProfScope ps(s->st, 0);
             GGS_HIP(launch_ga_variation(s->st, nullptr, nullptr, P, N, prm, d, c.seed, gen, (float*)s->off[onew].p,
@@ -1250,11 +1202,6 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
         }
         s->cur = nxt;
         s->n_curves += 1;
-        if (lpt) {
-            ProfScope pl(s->st, 3);
-            GGS_HIP(launch_lpt(s->st, (const int*)s->costs.p, nb * G, s->c->simds,
-                               s->lpt_add >= 0 ? s->lpt_add : lpt_cost_add(N), (int*)s->blkmap.p));
-        }
     } else {
         if ((rc = ga_flush(s))) return rc;
         ProfScope ps(s->st, 0);
@@ -1268,8 +1215,7 @@ int ga_generation(GaSession* s, int gen, int total, const ggs_ga_draws* hd) {
                                        (const int4*)s->bnds.p + (int64_t)b0 * N, nb, N, c.H, c.W,
                                        (const float4*)s->plan.p, (float*)s->partials.p, (const float*)s->wpart.p,
                                        c.fitness_mode, (const int*)s->order.p, s->fctr,
-                                       (float*)s->off_fits.p + b0, true, nullptr, nullptr,
-                                       lpt ? (const int*)s->blkmap.p : nullptr)))
+                                       (float*)s->off_fits.p + b0, true)))
         return rc;
     if (s->comm && per > 0) {   // one in-place all-gather of the shards' fitness scalars (RCCL, same stream)
         float* of = (float*)s->off_fits.p;
@@ -1291,6 +1237,7 @@ struct SaSession {
     ggs_ga_config cfg{};
     int N = 0, cap = 0, last_n = 0, nTiles = 0;
     bool incremental = false;   // measured slower at every SA config tried
+    int dirty_rule = 1;         // 1: a splat is changed when its raster record is; 0: its genes (GGS_SA_DIRTY_RULE)
     // cur_recs / cur_part describe the current state (create evaluates them, commit and
     // an incremental device run install them); a non-incremental ggs_sa_run may
     // accept neighbours without installing them
@@ -1331,7 +1278,8 @@ int sa_eval(SaSession* s, const float* G, int n, SplatRec* recs, int4* bnds, flo
     }
     if (dirty)
         GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, G, (const SplatRec*)s->cur_recs.p, recs, n,
-                             s->N, c.H, c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p));
+                             s->N, c.H, c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p, nullptr,
+                             s->dirty_rule));
     return raster_fitness(s->st, s->c->simds, recs, bnds, n, s->N, c.H, c.W, (const float4*)s->plan.p, part,
                           (const float*)s->wpart.p, c.fitness_mode, (const int*)s->order.p, s->fctr, fits, false,
                           dirty ? (const unsigned char*)s->dirty.p : nullptr, (const float*)s->cur_part.p);
@@ -1363,7 +1311,7 @@ void ga_free(GaSession* s) {
                       &s->src, &s->elite[0], &s->elite[1],
                       &s->target, &s->mask, &s->best_ind, &s->best_fit, &s->best_src, &s->best_upd,
                       &s->curves, &s->draws, &s->recs, &s->bnds, &s->partials, &s->plan, &s->wpart, &s->order,
-                      &s->fctr, &s->costs, &s->blkmap})
+                      &s->fctr})
         if (b->p) (void)hipFree(b->p);
     if (s->st) (void)hipStreamDestroy(s->st);
 }
@@ -1387,10 +1335,6 @@ int ggs_ga_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     ga_fill_log_bounds(&s->cfg);
     s->P = c.pop_size;
     s->N = c.n_splats;
-    if (const char* v = getenv("GGS_GA_LPT")) s->lpt = atoi(v) != 0;
-    if (const char* v = getenv("GGS_LPT_HEAD")) s->lpt_head = atoi(v);
-    if (const char* v = getenv("GGS_LPT_PK")) s->lpt_pk = atoi(v);
-    if (const char* v = getenv("GGS_LPT_ADD")) s->lpt_add = atoi(v);
     const size_t pb = sizeof(float) * 9 * (size_t)s->P * s->N, hw = (size_t)c.H * c.W;
     // what every rank of a sharded session must agree on (ggs_ga_set_comm checks it)
     s->fingerprint = hash_bytes(&s->cfg, sizeof s->cfg) * 0x9E3779B97F4A7C15ull ^
@@ -1551,6 +1495,7 @@ int ggs_sa_create(int32_t device, const ggs_ga_config* cfg, const float* target_
     ga_fill_log_bounds(&s->cfg);
     s->N = cfg->n_splats;
     s->cap = cfg->pop_size;
+    if (const char* v = getenv("GGS_SA_DIRTY_RULE")) s->dirty_rule = atoi(v) != 0;   // A/B: 0 = genes
     const size_t ib = sizeof(float) * 9 * (size_t)s->N, hw = (size_t)cfg->H * cfg->W;
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard dg(ctx->dev);
@@ -1787,7 +1732,7 @@ int ggs_sa_run(void* handle, int32_t first_it, int32_t n_its, int32_t total_iter
         if (s->incremental)
             GGS_HIP(launch_dirty(s->st, (const float*)s->curr.p, (const float*)s->nb.p,
                                  (const SplatRec*)s->cur_recs.p, (const SplatRec*)s->nb_recs.p, gcap, s->N, c.H,
-                                 c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p, live));
+                                 c.W, (unsigned char*)s->dirty.p, (unsigned*)s->counters.p, live, s->dirty_rule));
         {
             ProfScope ps(s->st, 1);
             GGS_HIP(launch_raster(s->st, 1, (const SplatRec*)s->nb_recs.p, (const int4*)s->nb_bnds.p, gcap, s->N,

@@ -271,44 +271,6 @@ __device__ void breed_stats(const BreedDev& br, int P, int N, const float* s_nf,
     }
 }
 
-// Per-strip raster cost of one offspring (launch_lpt's input; ggs_internal.h): each
-// splat adds, for every 128-row tile row its AABB spans, LPT_HEAD + LPT_PK x (row
-// pairs the raster walks there) to the 16-column strips its columns span — the
-// raster's cull test (x0 <= sx0 + 15, x1 >= sx0, the rows likewise) — as two
-// entries of a per-tile-row difference array in LDS; one wave per tile row then
-// prefix-sums it into cost[ty * cols + sx] (= the raster's strip index t * 4 + wv).
-__device__ __forceinline__ void strip_cost_add(const int4& bb, int H, int W, int cols, int head, int pk,
-                                               int* __restrict__ s_cd) {
-    constexpr int NPK = RASTER_TILE_H / 8;
-    const int x0 = min(max(bb.x, 0), W - 1), x1 = min(max(bb.y, x0), W - 1);
-    const int y0 = min(max(bb.z, 0), H - 1), y1 = min(max(bb.w, y0), H - 1);
-    for (int ty = y0 / RASTER_TILE_H; ty <= y1 / RASTER_TILE_H; ++ty) {
-        const int ty0 = ty * RASTER_TILE_H, dy0 = y0 - ty0, dy1 = y1 - ty0;
-        const int kA = max(dy0, 0) >> 3, kB = dy1 >= RASTER_TILE_H - 1 ? NPK - 1 : dy1 >> 3;
-        const int c = head + pk * (kB - kA + 1);
-        atomicAdd(&s_cd[ty * (cols + 1) + (x0 >> 4)], c);
-        atomicAdd(&s_cd[ty * (cols + 1) + (x1 >> 4) + 1], -c);
-    }
-}
-__device__ __forceinline__ void strip_cost_store(const int* __restrict__ s_cd, int rows, int cols, int* __restrict__ out) {
-    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-    for (int ty = threadIdx.x >> 6; ty < rows; ty += nw) {
-        int carry = 0;
-        for (int c0 = 0; c0 < cols; c0 += 64) {
-            const int c = c0 + lane;
-            int v = c < cols ? s_cd[ty * (cols + 1) + c] : 0;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int u = __shfl_up(v, d);
-                if (lane >= d) v += u;
-            }
-            v += carry;
-            if (c < cols) out[ty * cols + c] = v;
-            carry = __shfl(v, 63);
-        }
-    }
-}
-
 #ifndef GGS_VTIMING
 #define GGS_VTIMING 0             // diagnostic build: per-workgroup phase clocks (tools/probe/breed_timing.py)
 #endif
@@ -344,7 +306,6 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
     __shared__ float s_sizei;
     __shared__ int s_j, s_count;
     __shared__ int s_scan[VT / 64];
-    __shared__ int s_cd[BREED ? LPT_CD_MAX : 1];   // per-strip cost differences (launch_lpt)
     const int o = blockIdx.x;                  // offspring index
     GGS_VMARK(0);
     const int pair = o >> 1;
@@ -372,11 +333,6 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
     const float p = prm.mutpb;
     const int64_t ob = (int64_t)o * N;
     const int E = br.elite_k < 1 ? 1 : br.elite_k;
-    // this offspring's per-strip raster costs (single-round packing; uniform)
-    const bool cost_on = BREED && br.costs && o >= br.cost_o0 && o < br.cost_o0 + br.cost_n;
-    const int crows = lpt_rows(H), ccols = lpt_cols(W);
-    if (cost_on)
-        for (int i = tid; i < crows * (ccols + 1); i += VT) s_cd[i] = 0;
 
     if (N <= VT) {
         // One splat per thread (s = tid).  Phase A issues everything that does not
@@ -558,14 +514,8 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
                 encode_row(g, row);
                 const SplatRec r = make_rec(preprocess_row(row, H, W, k_sigma));
                 recs[ob + sp] = r;
-                const int4 bb = rec_bounds(r);
-                bnds[ob + sp] = bb;
-                if (cost_on) strip_cost_add(bb, H, W, ccols, br.cost_head, br.cost_pk, s_cd);
+                bnds[ob + sp] = rec_bounds(r);
             }
-        }
-        if (cost_on) {
-            __syncthreads();
-            strip_cost_store(s_cd, crows, ccols, br.costs + (int64_t)(o - br.cost_o0) * crows * ccols);
         }
         if (BREED) {            // gather: row o of P_g and its fitness, for the generation after
             float* __restrict__ to = br.pop_next + (int64_t)o * N * 9;
@@ -710,14 +660,8 @@ ga_variation_kernel(const float* __restrict__ pop, const float* __restrict__ fit
             encode_row(O + (int64_t)s * 9, row);
             const SplatRec r = make_rec(preprocess_row(row, H, W, k_sigma));
             recs[(int64_t)o * N + s] = r;
-            const int4 bb = rec_bounds(r);
-            bnds[(int64_t)o * N + s] = bb;
-            if (cost_on) strip_cost_add(bb, H, W, ccols, br.cost_head, br.cost_pk, s_cd);
+            bnds[(int64_t)o * N + s] = rec_bounds(r);
         }
-    }
-    if (cost_on) {
-        __syncthreads();
-        strip_cost_store(s_cd, crows, ccols, br.costs + (int64_t)(o - br.cost_o0) * crows * ccols);
     }
 }
 

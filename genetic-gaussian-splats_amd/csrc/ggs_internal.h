@@ -68,48 +68,22 @@ struct FinFused {
     int mode = 0;                     // GGS_FIT_*
 };
 // simds: SIMDs of the launch's device (DevCtx::simds; 0 = unknown: no single-round
-// reordering).  blk_map (device, may be null): block -> strip item b * G + g
-// (G = raster_tiles * 4) from launch_lpt; replaces the centre-first order.
+// reordering).
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty = nullptr,
                          const float* clean = nullptr, const int* live = nullptr, const FinFused* fin = nullptr,
-                         int simds = 0, const int* blk_map = nullptr);
+                         int simds = 0);
 // SIMDs (CUs x 4) of HIP device `dev`, 0 if unknown.
 int device_simds(int dev);
 
-// ---- single-round packing by exact strip cost (device GA) ---------------------
-// A raster launch of n strip-waves with 2S < n <= 3S (S = SIMDs) runs in one
-// round: every wave is resident from the start and blocks r, r + S, r + 2S share
-// SIMD r, whose VALU they split (docs/EXPERIMENTS.md §14), so the launch ends with
-// the largest per-SIMD SUM of strip costs.  The breed computes every evaluated
-// candidate's per-strip cost (the raster's visit geometry: LPT_HEAD per visit +
-// LPT_PK per row pair walked) and launch_lpt packs the n strips three to a SIMD
-// (largest first, in rounds: the second round reversed, the third to the least
-// loaded SIMDs), writing the raster's block -> strip map.  Order only: a strip's
-// bits never depend on the block that runs it.
-constexpr int RASTER_TILE_W = 64;
-#ifndef GGS_TILE_H
-#define GGS_TILE_H 128            // (probe builds may override; ggs_kernels.hip)
-#endif
-constexpr int RASTER_TILE_H = GGS_TILE_H;
-constexpr int LPT_MAX = 4096;     // strips per packed launch
-constexpr int LPT_CD_MAX = 4096;  // breed LDS: tile rows x (strip columns + 1) cost-difference cells
-constexpr int LPT_HEAD = 30, LPT_PK = 7, LPT_CULL64 = 12, LPT_EPI = 260;   // VALU-slot model (tools/probe/sched_model.py)
-__host__ __device__ inline int lpt_cols(int W) { return 4 * ((W + RASTER_TILE_W - 1) / RASTER_TILE_W); }
-__host__ __device__ inline int lpt_rows(int H) { return (H + RASTER_TILE_H - 1) / RASTER_TILE_H; }
-inline bool lpt_applies(int n, int simds, int H, int W) {
-    return simds > 0 && n > 2 * simds && n <= 3 * simds && n <= LPT_MAX &&
-           lpt_rows(H) * (lpt_cols(W) + 1) <= LPT_CD_MAX;
-}
-// cost [n] (breed output, per strip), + cost_add each -> map [n] (a permutation of [0, n))
-hipError_t launch_lpt(hipStream_t st, const int* cost, int n, int simds, int cost_add, int* map);
-inline int lpt_cost_add(int N) { return LPT_EPI + LPT_CULL64 * ((N + 63) / 64); }
-// Strips touched by splats that differ between `nb` [n][N][9] and `curr` [N][9]
-// (old AABB from cur_recs, new from nb_recs) -> dirty [n][tiles][4] (zeroed first).
+// Strips touched by splats that differ between the neighbours and the current
+// state (old AABB from cur_recs, new from nb_recs) -> dirty [n][tiles][4] (zeroed
+// first).  rule 1: a splat differs when its raster record does (nb_recs [n][N] vs
+// cur_recs [N]); rule 0: when its genes do (nb [n][N][9] vs curr [N][9]).
 hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, const SplatRec* cur_recs,
                         const SplatRec* nb_recs, int n, int N, int H, int W, unsigned char* dirty,
-                        unsigned* n_changed, const int* live = nullptr);
+                        unsigned* n_changed, const int* live = nullptr, int rule = 1);
 // Target plan for the fitness epilogue (built once per target/mask/mode/beta).
 // wblock (plan_wsum_bytes): the plan's Sum w as a double, then per-wave sums.
 hipError_t launch_plan(hipStream_t st, const float* target, const float* mask, int mode, float beta,
@@ -249,11 +223,6 @@ struct BreedDev {               // the fused breed (launch_ga_variation with br 
     double* curves_row;         // [3] best, mean, median of P_g
     GaBestDev best;
     int elite_k;
-    // single-round packing (launch_lpt): offspring [cost_o0, cost_o0 + cost_n) write
-    // their per-strip costs to costs[(o - cost_o0) * G + g] (null: none)
-    int* costs = nullptr;
-    int cost_o0 = 0, cost_n = 0;
-    int cost_head = 0, cost_pk = 0;   // LPT_HEAD / LPT_PK (a session may override them: GGS_LPT_HEAD / _PK)
 };
 hipError_t launch_ga_variation(hipStream_t st, const float* pop, const float* fits, int P, int N,
                                const GaParamsDev& prm, const GaDrawsDev& d, uint64_t seed, int gen,

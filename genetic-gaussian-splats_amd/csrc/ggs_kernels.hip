@@ -321,8 +321,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
               float bg_r, float bg_g, float bg_b, float* __restrict__ img,
               const float4* __restrict__ plan, float* __restrict__ partials,
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
-              const float* __restrict__ clean, const int* __restrict__ live, int CH, FinFused fin, int simds,
-              const int* __restrict__ blk_map) {
+              const float* __restrict__ clean, const int* __restrict__ live, int CH, FinFused fin, int simds) {
     constexpr bool DS = GGS_DEPTH_SPLIT && MODE == 1 && !SAT;
     __shared__ int lists[DS ? 2 : WPB][CAP];   // per-wave strip lists (descending splat index)
 
@@ -349,46 +348,36 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
     // candidate; groups go central (heavy) first to shorten the grid's tail.
     // Large launches run in candidate chunks of CH (all groups of one chunk, then
     // the next), so a chunk's records stay cached while its groups run
-    int b, grp;
-    if (blk_map) {
-        // single-round launch packed by exact strip cost (lpt_kernel): this block's
-        // (candidate, strip) from the map, a permutation of the launch's strips
-        const int it = blk_map[blockIdx.x];
-        const int G = nTiles * SPB;
-        b = it / G;
-        grp = it - b * G;
-    } else {
-        int idx = blockIdx.x, b0 = 0, Bc = B;
-        // A launch of 2-3 strip-waves per SIMD runs in one round: every wave is
-        // resident from the start and the three sharing a SIMD (blocks r, r + S,
-        // r + 2S, S = SIMDs) split its VALU, so the SIMD ends with the SUM of their
-        // work (docs/EXPERIMENTS.md §14).  The middle third runs reversed: the
-        // heaviest (central) strips then share a SIMD with the lightest of the
-        // middle third instead of its heaviest (a boustrophedon over the expected
-        // cost order; the bits do not depend on the order).  Shipped GA launch
-        // (24 x 128 strips) raster -1.45 %; with two waves per SIMD (a lone 2048^2
-        // SA neighbour) the pairing measured +1.05 %, so only above 2S (EXP §15)
-        if (simds > 0) {
-            const int n = B * nTiles * SPB;
-            if (n > 2 * simds && n <= 3 * simds && idx >= simds && idx < 2 * simds) idx = 3 * simds - 1 - idx;
-        }
-        if (B > CH) {
-            const int per = CH * nTiles * SPB;
-            const int c = idx / per;
-            idx -= c * per;
-            b0 = c * CH;
-            Bc = min(CH, B - b0);
-        }
-        const int gi = idx / Bc;
-        grp = tile_order ? tile_order[gi] : gi;
-        // candidates rotate by one per group: with B % 8 == 0 a fixed b would stay on
-        // one XCD (blocks go round-robin to the 8 XCDs) and per-XCD work would be the
-        // sum of 16 candidates' costs (tools/probe/wave_timing.py: XCD end times 197-207 us)
-        // ... for the large-N instances only every 2^XCD_SHIFT groups: blocks B apart
-        // (the next group's block in the same XCD slot) then run the same candidate,
-        // whose records stay in that XCD's caches across 8 groups (see XCD_SHIFT)
-        b = b0 + (int)((idx + (gi >> (SAT ? XCD_SHIFT : 0))) % Bc);
+    int idx = blockIdx.x, b0 = 0, Bc = B;
+    // A launch of 2-3 strip-waves per SIMD runs in one round: every wave is
+    // resident from the start and the three sharing a SIMD (blocks r, r + S,
+    // r + 2S, S = SIMDs) split its VALU, so the SIMD ends with the SUM of their
+    // work (docs/EXPERIMENTS.md §14).  The middle third runs reversed: the
+    // heaviest (central) strips then share a SIMD with the lightest of the
+    // middle third instead of its heaviest (a boustrophedon over the expected
+    // cost order; the bits do not depend on the order).  Shipped GA launch
+    // (24 x 128 strips) raster -1.45 %; with two waves per SIMD (a lone 2048^2
+    // SA neighbour) the pairing measured +1.05 %, so only above 2S (EXP §15)
+    if (simds > 0) {
+        const int n = B * nTiles * SPB;
+        if (n > 2 * simds && n <= 3 * simds && idx >= simds && idx < 2 * simds) idx = 3 * simds - 1 - idx;
     }
+    if (B > CH) {
+        const int per = CH * nTiles * SPB;
+        const int c = idx / per;
+        idx -= c * per;
+        b0 = c * CH;
+        Bc = min(CH, B - b0);
+    }
+    const int gi = idx / Bc;
+    const int grp = tile_order ? tile_order[gi] : gi;
+    // candidates rotate by one per group: with B % 8 == 0 a fixed b would stay on
+    // one XCD (blocks go round-robin to the 8 XCDs) and per-XCD work would be the
+    // sum of 16 candidates' costs (tools/probe/wave_timing.py: XCD end times 197-207 us)
+    // ... for the large-N instances only every 2^XCD_SHIFT groups: blocks B apart
+    // (the next group's block in the same XCD slot) then run the same candidate,
+    // whose records stay in that XCD's caches across 8 groups (see XCD_SHIFT)
+    const int b = b0 + (int)((idx + (gi >> (SAT ? XCD_SHIFT : 0))) % Bc);
     const int t = grp / SPB;
     const int wv = (grp % SPB) * WPB + wib;           // strip 0..3 of the tile
     const int tx0 = (t % nTX) * TILE;
@@ -1008,10 +997,14 @@ size_t plan_wsum_bytes(int H, int W) { return 16 + sizeof(float) * 4 * PLAN_Q * 
 // ---------------------------------------------------------------------------
 // dirty strips (incremental SA evaluation, SURVEY.md §8f #4 / annealing.py:121-146)
 // ---------------------------------------------------------------------------
-// Thread per (neighbour b, splat i): if any of the 9 genes differ from the
-// current state (bitwise), every strip the splat's old or new AABB touches is
-// marked dirty for neighbour b.  Strips no changed splat touches keep their
-// cull list and blend order, so their partial is the current state's.
+// Thread per (neighbour b, splat i): if the splat changed, every strip its old or
+// new AABB touches is marked dirty for neighbour b.  Strips no changed splat
+// touches keep their cull list and blend order, so their partial is the current
+// state's.  "Changed" (rule): 1 = its 64-B raster record differs (the record holds
+// everything the raster reads of a splat, its AABB included, so an unchanged
+// record cannot move any strip's bits; a theta moved by an ulp by the double
+// wrap_angle of genetic.py:71 + utils.py:43 often leaves the record as it was);
+// 0 = any of its 9 genes differ bitwise (the round-2 rule).
 __device__ __forceinline__ void mark_strips(const SplatRec& r, int nTX, unsigned char* __restrict__ d) {
     for (int ty = r.y0 / TILE_H; ty <= r.y1 / TILE_H; ++ty)
         for (int sx = r.x0 / 16; sx <= r.x1 / 16; ++sx) d[(ty * nTX + (sx >> 2)) * 4 + (sx & 3)] = 1;
@@ -1021,15 +1014,25 @@ __global__ void __launch_bounds__(256)
 dirty_kernel(const float* __restrict__ curr, const float* __restrict__ nb,
              const SplatRec* __restrict__ cur_recs, const SplatRec* __restrict__ nb_recs, int n, int N,
              int nTX, int nTiles, unsigned char* __restrict__ dirty, unsigned* __restrict__ n_changed,
-             const int* __restrict__ live) {
+             const int* __restrict__ live, int rule) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)(live ? min(*live, n) : n) * N) return;
     const int b = (int)(idx / N), i = (int)(idx % N);
-    const unsigned* a = reinterpret_cast<const unsigned*>(curr + (int64_t)i * 9);
-    const unsigned* c = reinterpret_cast<const unsigned*>(nb + idx * 9);
     unsigned diff = 0;
+    if (rule == 1) {
+        const uint4* a = reinterpret_cast<const uint4*>(cur_recs + i);
+        const uint4* c = reinterpret_cast<const uint4*>(nb_recs + idx);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) diff |= a[k] ^ c[k];
+        for (int k = 0; k < 4; ++k) {
+            const uint4 x = a[k], y = c[k];
+            diff |= (x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w);
+        }
+    } else {
+        const unsigned* a = reinterpret_cast<const unsigned*>(curr + (int64_t)i * 9);
+        const unsigned* c = reinterpret_cast<const unsigned*>(nb + idx * 9);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) diff |= a[k] ^ c[k];
+    }
     if (!diff) return;
     unsigned char* d = dirty + (int64_t)b * nTiles * 4;
     mark_strips(cur_recs[i], nTX, d);
@@ -1039,7 +1042,7 @@ dirty_kernel(const float* __restrict__ curr, const float* __restrict__ nb,
 
 hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, const SplatRec* cur_recs,
                         const SplatRec* nb_recs, int n, int N, int H, int W, unsigned char* dirty,
-                        unsigned* n_changed, const int* live) {
+                        unsigned* n_changed, const int* live, int rule) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     hipError_t e = hipMemsetAsync(dirty, 0, (size_t)n * nTiles * 4, st);
@@ -1047,7 +1050,7 @@ hipError_t launch_dirty(hipStream_t st, const float* curr, const float* nb, cons
     const int64_t tot = (int64_t)n * N;
     if (tot == 0) return hipSuccess;
     hipLaunchKernelGGL(dirty_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, curr, nb,
-                       cur_recs, nb_recs, n, N, nTX, nTiles, dirty, n_changed, live);
+                       cur_recs, nb_recs, n, N, nTX, nTiles, dirty, n_changed, live, rule);
     return hipGetLastError();
 }
 
@@ -1153,8 +1156,8 @@ int raster_chunk(int N) {
     return ch < 8 ? 8 : (int)ch;
 }
 
-// SIMDs (CUs x 4) of HIP device `dev`, for the single-round block order and the
-// LPT packing; 0 if unknown (no reordering).  Callers pass their context's device
+// SIMDs (CUs x 4) of HIP device `dev`, for the single-round block order; 0 if
+// unknown (no reordering).  Callers pass their context's device
 // (DevCtx::simds), not the current one.
 int device_simds(int dev) {
     int cus = 0;
@@ -1165,7 +1168,7 @@ int device_simds(int dev) {
 hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const int4* bnds, int B, int N, int H, int W,
                          const float bg[3], float* img, const float4* plan, float* partials,
                          const int* tile_order, const unsigned char* dirty, const float* clean,
-                         const int* live, const FinFused* fin, int simds, const int* blk_map) {
+                         const int* live, const FinFused* fin, int simds) {
     int nTX;
     const int nTiles = raster_tiles(H, W, &nTX);
     const dim3 grid((unsigned)((int64_t)B * nTiles * SPB)), block(NT);
@@ -1178,117 +1181,13 @@ hipError_t launch_raster(hipStream_t st, int mode, const SplatRec* recs, const i
     // of its code (a runtime test left the SA raster 1 % slower than round 3's)
 #define GGS_RASTER(M, S, F)                                                                    \
     hipLaunchKernelGGL((raster_kernel<M, S, F>), grid, (M) ? block_f : block, 0, st, recs, bnds, B, N, H, W, nTX, nTiles, \
-                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH, ff, simds, blk_map)
+                       bg[0], bg[1], bg[2], img, plan, partials, tile_order, dirty, clean, live, CH, ff, simds)
     // the saturation check only where strip lists can grow long (N > SAT_MIN_SPLATS);
     // at the bench's 256 splats the kernel without it is the faster code (+1.6 %)
     if (mode == 0) { if (!sat) GGS_RASTER(0, false, false); else GGS_RASTER(0, true, false); }   // image
     else if (!ff.ctr) { if (!sat) GGS_RASTER(1, false, false); else GGS_RASTER(1, true, false); }   // fitness
     else { if (!sat) GGS_RASTER(1, false, true); else GGS_RASTER(1, true, true); }  // + folded finalize
 #undef GGS_RASTER
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// single-round packing by exact strip cost (ggs_internal.h, launch_lpt)
-// ---------------------------------------------------------------------------
-// One workgroup of 1,024 threads.  The n strips (2S < n <= 3S) are ordered by
-// cost, largest first (a 2,048-bucket counting sort: the order inside a bucket,
-// 1/2,048 of the largest cost wide, is arbitrary), then packed in rounds: SIMD j
-// takes strip j of the first S and strip 2S - 1 - j of the second S (the largest
-// of round two to the lightest of round one), and the remaining n - 2S strips go,
-// largest first, to the SIMDs in increasing order of load.  Hardware SIMD r runs
-// blocks r, r + S, r + 2S, and only r < n - 2S has a third block, so r is the
-// r-th least loaded SIMD.  Model (tools/probe/sched_model.py costs, the shipped
-// GA launch): max per-SIMD sum 1.189x -> 1.044x the mean.
-constexpr int LPT_NB = 2048, LPT_NT = 1024;
-
-__device__ __forceinline__ int lpt_block_max(int v, int* red) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    int m = 0;
-    for (int q = 0; q < LPT_NT / 64; ++q) m = max(m, red[q]);
-    __syncthreads();
-    return m;
-}
-
-// exclusive prefix sum of a[0, 2 * LPT_NT) in place
-__device__ __forceinline__ void lpt_block_scan(int* a, int* red) {
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int x0 = a[2 * t], x1 = a[2 * t + 1];
-    int v = x0 + x1;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int u = __shfl_up(v, d);
-        if (lane >= d) v += u;
-    }
-    if (lane == 63) red[w] = v;
-    __syncthreads();
-    int off = 0;
-    for (int q = 0; q < w; ++q) off += red[q];
-    const int ex = off + v - (x0 + x1);
-    a[2 * t] = ex;
-    a[2 * t + 1] = ex + x0;
-    __syncthreads();
-}
-
-// out[0, n) = items [0, n) by bucket key(i) ascending (ties in arbitrary order)
-template <class Key>
-__device__ __forceinline__ void lpt_bucket_sort(int n, Key key, int* hist, int* red, int* out) {
-    for (int i = threadIdx.x; i < LPT_NB; i += LPT_NT) hist[i] = 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += LPT_NT) atomicAdd(&hist[key(i)], 1);
-    __syncthreads();
-    lpt_block_scan(hist, red);
-    for (int i = threadIdx.x; i < n; i += LPT_NT) out[atomicAdd(&hist[key(i)], 1)] = i;
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(LPT_NT)
-lpt_kernel(const int* __restrict__ cost, int n, int S, int cost_add, int* __restrict__ map) {
-    __shared__ int s_c[LPT_MAX];        // strip costs
-    __shared__ int s_sorted[LPT_MAX];   // strips, largest cost first
-    __shared__ int s_load[LPT_MAX / 2]; // SIMD loads after two rounds (S < n / 2)
-    __shared__ int s_asc[LPT_MAX / 2];  // SIMDs by load, least first
-    __shared__ int s_hist[LPT_NB];
-    __shared__ int s_red[LPT_NT / 64];
-    if (n <= 2 * S || n > 3 * S || n > LPT_MAX) {    // (the host checks lpt_applies): identity
-        for (int i = threadIdx.x; i < n; i += LPT_NT) map[i] = i;
-        return;
-    }
-    int m = 0;
-    for (int i = threadIdx.x; i < n; i += LPT_NT) {
-        const int c = max(cost[i], 0) + cost_add;
-        s_c[i] = c;
-        m = max(m, c);
-    }
-    const int cmax = max(lpt_block_max(m, s_red), 1);
-    lpt_bucket_sort(n, [&](int i) { return (LPT_NB - 1) - (int)((int64_t)s_c[i] * (LPT_NB - 1) / cmax); },
-                    s_hist, s_red, s_sorted);
-    m = 0;
-    for (int j = threadIdx.x; j < S; j += LPT_NT) {
-        const int l = s_c[s_sorted[j]] + s_c[s_sorted[2 * S - 1 - j]];
-        s_load[j] = l;
-        m = max(m, l);
-    }
-    const int lmax = max(lpt_block_max(m, s_red), 1);
-    lpt_bucket_sort(S, [&](int j) { return (int)((int64_t)s_load[j] * (LPT_NB - 1) / lmax); },
-                    s_hist, s_red, s_asc);
-    const int third = n - 2 * S;
-    for (int r = threadIdx.x; r < S; r += LPT_NT) {
-        const int j = s_asc[r];
-        map[r] = s_sorted[j];
-        map[r + S] = s_sorted[2 * S - 1 - j];
-        if (r < third) map[r + 2 * S] = s_sorted[2 * S + r];
-    }
-}
-
-hipError_t launch_lpt(hipStream_t st, const int* cost, int n, int simds, int cost_add, int* map) {
-    if (n <= 0) return hipSuccess;
-    if (simds > LPT_NT * 2) return hipErrorInvalidValue;   // s_load / s_asc hold 2,048 SIMDs
-    hipLaunchKernelGGL(lpt_kernel, dim3(1), dim3(LPT_NT), 0, st, cost, n, simds, cost_add, map);
     return hipGetLastError();
 }
 

@@ -8,7 +8,7 @@ from ._lib import (GGS_FIT_BOOST, GGS_FIT_NONE, GGS_FIT_WEIGHTED, GGSDeviceError
                    GGSError, GGSInputError, LIB_PATH, ensure_init, lib, runtime_info, select_devices)
 from .parallel import RcclGather  # noqa: F401
 from .api import (TargetPlan, as_f32, encode, fitness, fitness_device,  # noqa: F401
-                  fitness_population, lpt_pack, preprocess, profile_enable, profile_read, profile_reset,
+                  fitness_population, preprocess, profile_enable, profile_read, profile_reset,
                   render, render_device)
 
 __version__ = "0.1.0"

@@ -61,7 +61,6 @@ SIGNATURES = {
                                      C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_float,
                                      C.c_int32, C.c_int32, C.c_float, C.c_void_p]),
     "ggs_detmath_eval": (C.c_int, [C.c_int32, _f32p, _f32p, C.c_int64, _f32p]),
-    "ggs_lpt_pack": (C.c_int, [_i32p, C.c_int32, C.c_int32, C.c_int32, _i32p]),
     "ggs_profile_enable": (C.c_int, [C.c_int32]),
     "ggs_profile_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "ggs_profile_reset": (None, []),

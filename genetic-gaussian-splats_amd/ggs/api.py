@@ -256,16 +256,3 @@ def profile_read(kernel: str):
 def profile_reset() -> None:
     lib.ggs_profile_reset()
 
-
-def lpt_pack(costs, simds: int, cost_add: int = 0) -> np.ndarray:
-    """Single-round packing (include/ggs.h ggs_lpt_pack, the device GA's kernel):
-    per-strip costs of one raster launch with 2*simds < n <= 3*simds strips ->
-    block map (block r + k*simds runs strip map[r + k*simds]; blocks r, r + simds,
-    r + 2*simds share SIMD r)."""
-    c = np.ascontiguousarray(np.asarray(costs, np.int32).ravel())
-    out = np.empty(c.size, np.int32)
-    if c.size:
-        _lib.ensure_init()
-        check(lib.ggs_lpt_pack(c.ctypes.data_as(_lib._i32p), int(c.size), int(simds), int(cost_add),
-                               out.ctypes.data_as(_lib._i32p)), "ggs_lpt_pack")
-    return out

@@ -103,15 +103,6 @@ int ggs_preprocess(const float* genomes, int64_t S, int32_t C, int32_t H, int32_
  * 4 sqrt (correctly rounded), 5 x[i] / y[i] (correctly rounded). */
 int ggs_detmath_eval(int32_t fn, const float* x, const float* y, int64_t n, float* out);
 
-/* Single-round packing (the device GA's raster launch of n strip-waves with
- * 2*simds < n <= 3*simds, at most 4,096): costs[i] (+ cost_add) of strip i ->
- * map[r + k*simds] = the strip block r + k*simds runs, a permutation of [0, n)
- * that packs three strips per SIMD (blocks r, r + simds, r + 2*simds share SIMD
- * r), largest first in rounds.  Order only (the raster's bits never depend on
- * it).  Runs the device kernel the GA uses; replaces the centre-first grid order
- * of render.py:240-251's single launch for these shapes. */
-int ggs_lpt_pack(const int32_t* costs, int32_t n, int32_t simds, int32_t cost_add, int32_t* map);
-
 /* ---- device-pointer API (inputs resident in HBM) ----------------------------
  * Same semantics as the host API on one device; all pointers are device
  * pointers on `device`; work is enqueued on `stream` (a hipStream_t, NULL =
@@ -308,7 +299,7 @@ int ggs_comm_allgather_host(void* comm, const float* send, float* recv, int64_t 
 int ggs_comm_barrier(void* comm);
 
 /* ---- per-kernel timing (HIP events on the launch stream) --------------------
- * When enabled, every launch of "prep", "raster", "finalize" and "lpt" is bracketed
+ * When enabled, every launch of "prep", "raster" and "finalize" is bracketed
  * by hipEvents; ggs_profile_read synchronises those events and returns the
  * accumulated milliseconds and launch count for the named kernel (a finalize
  * folded into the raster counts as raster time, no finalize launch). */

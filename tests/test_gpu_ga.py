@@ -155,15 +155,12 @@ init = ga.new_population(P, N, H, W, 3.0, 0.1, np.random.default_rng(0))
 cfg = dict(mut_sigma_max={"xy": 0.1, "alog": 0.5, "blog": 0.5, "theta": 0.3, "rgb": 25.0, "alpha": 25.0},
            mut_sigma_min={"xy": 0.01, "alog": 0.05, "blog": 0.05, "theta": 0.025, "rgb": 2.0, "alpha": 2.0},
            schedule="cosine")
-import ggs
-ggs.profile_enable(True)
 dga = DeviceGA(t, m, init, tour_k=2, elite_k=8, cxpb=0.05, mutpb=0.05, min_scale_splats=3.0,
                max_scale_splats=0.1, seed=1, **cfg)
 dga.run(1, 25, 25)
 st = dga.read()
 np.savez(sys.argv[2], population=st["population"], fitness=st["fitness"], best=st["best"],
-         best_fit=st["best_fit"], **{"c_" + k: np.asarray(v) for k, v in st["curves"].items()},
-         lpt_launches=np.int64(ggs.profile_read("lpt")[1]))
+         best_fit=st["best_fit"], **{"c_" + k: np.asarray(v) for k, v in st["curves"].items()})
 """
 
 
@@ -174,30 +171,21 @@ def test_device_ga_fused_breed_equals_unfused(tmp_path, P, N):
     raster against its own launch (GGS_UNFUSED_FINALIZE=1), at the bench workload
     and at the reference's shipped run (config.py: 512 splats, pop 32), 25
     generations of Philox draws in one run: identical populations, fitness, best
-    and curves.  At the shipped run (24 evaluated x 128 strips = one round on
-    MI355X's 1,024 SIMDs) GGS_GA_LPT=1 packs the raster by exact strip cost
-    (launch_lpt; off by default): the same bits either way."""
+    and curves (N = 1100: the generic breed path, several splats per thread)."""
     import os
     import subprocess
     import sys
     pkg = os.path.dirname(os.path.dirname(ggs.__file__))
     out = {}
     for tag, env in (("fused", {}), ("unfused", {"GGS_GA_UNFUSED": "1"}),
-                     ("unfused_fin", {"GGS_UNFUSED_FINALIZE": "1"}), ("lpt", {"GGS_GA_LPT": "1"})):
+                     ("unfused_fin", {"GGS_UNFUSED_FINALIZE": "1"})):
         path = str(tmp_path / f"{tag}.npz")
         subprocess.run([sys.executable, "-c", _FUSED_SCRIPT, pkg, path, str(P), str(N)], check=True, timeout=300,
                        env=dict(os.environ, **env))
         out[tag] = np.load(path)
     for k in out["fused"].files:
-        if k == "lpt_launches":
-            continue
         np.testing.assert_array_equal(out["fused"][k], out["unfused"][k], err_msg=k)
         np.testing.assert_array_equal(out["fused"][k], out["unfused_fin"][k], err_msg=k)
-        np.testing.assert_array_equal(out["fused"][k], out["lpt"][k], err_msg=k)
-    assert int(out["fused"]["lpt_launches"]) == 0 and int(out["unfused"]["lpt_launches"]) == 0
-    if P == 32:      # one round of strip-waves on a 256-CU MI355X: packed every fused generation
-        # (N = 1100: the generic breed path, several splats per thread, writes the costs)
-        assert int(out["lpt"]["lpt_launches"]) == 24, int(out["lpt"]["lpt_launches"])
 
 
 def test_device_ga_sessions_concurrent_uneven_load_equal_solo():
@@ -351,6 +339,29 @@ def test_device_sa_incremental_equals_full_rerender(H, W, N, mutpb, boost):
     assert f1 == f0 and s1["curves"] == s0["curves"]
     assert s1["stats"]["proposed"] == s1["stats"]["evaluated"] > 0
     assert 0 < s1["stats"]["changed_splats"] <= s1["stats"]["proposed"] * N
+
+
+def test_device_sa_dirty_rules_equal_full_rerender(monkeypatch):
+    """The two dirty-splat rules (GGS_SA_DIRTY_RULE, read at session creation):
+    a splat is changed when its raster record differs (1, the default) or when any
+    gene differs bitwise (0).  Both runs equal the full re-render bit for bit; the
+    record rule never marks more splats (an unchanged record renders the same)."""
+    H = W = 256
+    N = 300
+    target, _, _ = _problem(H, W, 21)
+    init = ga.new_population(1, N, H, W, MIN_S, MAX_S, np.random.default_rng(21))[0]
+    kw = dict(mutpb=0.01, iterations=10, tries_per_iter=6, temp0=1e-3, backend="device", seed=19,
+              init_individual=init)
+    b0, f0, s0 = _sa(target, H, W, N, incremental=False, **kw)
+    changed = {}
+    for rule in ("0", "1"):
+        monkeypatch.setenv("GGS_SA_DIRTY_RULE", rule)
+        b, f, st = _sa(target, H, W, N, incremental=True, **kw)
+        np.testing.assert_array_equal(b, b0)
+        np.testing.assert_array_equal(st["current"], s0["current"])
+        assert f == f0 and st["curves"] == s0["curves"]
+        changed[rule] = st["stats"]["changed_splats"]
+    assert 0 < changed["1"] <= changed["0"], changed
 
 
 @pytest.mark.parametrize("H,W,N,tries,spec,inc,iters", [(40, 40, 17, 4, None, False, 9),

@@ -97,10 +97,10 @@ if a.backend == "device":
         dga.read()
         ggs.profile_enable(False)
         kern = {}
-        for name, k in (("breed", "prep"), ("raster", "raster"), ("finalize", "finalize"), ("lpt", "lpt")):
+        for name, k in (("breed", "prep"), ("raster", "raster"), ("finalize", "finalize")):
             ms, n = ggs.profile_read(k)
             kern[name + "_us"] = round(ms * 1e3 / max(n, 1), 2)
-        kern["launches"] = {"raster": ggs.profile_read("raster")[1], "lpt": ggs.profile_read("lpt")[1]}
+        kern["launches"] = {"raster": ggs.profile_read("raster")[1]}
     if rank == 0:
         print(json.dumps({"metric": "GA generations/s (device-resident)", "value": round(a.gens / dt, 2),
                           "config": dict(config, n_gpus=world, sharded=dist is not None),
