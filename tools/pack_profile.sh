@@ -14,12 +14,15 @@ for p in fetch write sq wait; do
     mkdir -p "$DST/pmc_$p"
     python3 - "$SRC/pmc_$p/run_counter_collection.csv" "$DST/pmc_$p/run_counter_collection.csv" <<'PY'
 import csv, sys
+import os
 # the raster rows of the last 1,500 raster dispatches (a late-SA loop profiles
-# ~14k; the summary's means were taken over all of them on the box)
+# ~14k; the summary's means were taken over all of them on the box), or with
+# PROF_RASTER_GRID only those of that grid size (what the summary averaged)
+gf = int(os.environ.get("PROF_RASTER_GRID", "0") or 0)
 with open(sys.argv[1]) as f:
     r = csv.DictReader(f)
     fields = r.fieldnames
-    rows = [row for row in r if "raster_kernel" in row["Kernel_Name"]]
+    rows = [row for row in r if "raster_kernel" in row["Kernel_Name"] and (not gf or int(row["Grid_Size"]) == gf)]
 keep = set(sorted({int(row["Dispatch_Id"]) for row in rows})[-1500:])
 with open(sys.argv[2], "w", newline="") as g:
     w = csv.DictWriter(g, fieldnames=fields)

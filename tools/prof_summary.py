@@ -36,10 +36,45 @@ if os.path.exists(trace) and os.environ.get("PROF_BENCH_PASS") == "1":
     if len(dur) >= steps:
         out["raster_profile_pass_avg_us"] = sum(dur[-steps:]) / steps
         out["raster_dispatches"] = len(dur)
+# PROF_RASTER_GRID=<threads>: the raster's counters (and a trace average) over the
+# dispatches of that grid size only — a loop whose launches vary in width (the SA
+# device loop: one grid per round width) is summarised for one width, e.g. the
+# late regime's 16-neighbour rounds (16 x 2,048 strip-waves x 64 = 2,097,152)
+grid_f = int(os.environ.get("PROF_RASTER_GRID", "0") or 0)
+
+
+def _grid(r):
+    g = r.get("Grid_Size")
+    if g is None:
+        g = int(r.get("Grid_Size_X", 0) or 0) * int(r.get("Grid_Size_Y", 1) or 1) * int(r.get("Grid_Size_Z", 1) or 1)
+    return int(g)
+
+
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
+grids_seen = collections.Counter()
 for f in glob.glob(os.path.join(root, "pmc_*", "run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        k = r["Kernel_Name"].split("(")[0]
+        if grid_f and "raster_kernel" in k:
+            if "sq" in os.path.basename(os.path.dirname(f)) and r["Counter_Name"] == "SQ_WAVES":
+                grids_seen[_grid(r)] += 1
+            if _grid(r) != grid_f:
+                continue
+        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+if grid_f:
+    tr = os.path.join(root, "trace", "run_kernel_trace.csv")
+    durs = []
+    if os.path.exists(tr):
+        for r in csv.DictReader(open(tr)):
+            if "raster_kernel" in r.get("Kernel_Name", "") and _grid(r) == grid_f:
+                durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out["raster_grid_filter"] = {
+        "grid_threads": grid_f, "strip_waves": grid_f // 64,
+        "pmc_dispatches_by_grid_threads": dict(sorted(grids_seen.items())),
+        "pmc_dispatches_kept": grids_seen.get(grid_f, 0),
+        "trace_dispatches": len(durs),
+        "trace_avg_us": (sum(durs) / len(durs)) if durs else None,
+        "note": "counters of the raster kernel are means over the dispatches of this grid size only"}
 for k, cs in agg.items():
     out["counters"][k] = {c: sum(v) / len(v) for c, v in cs.items()}
 rasters = sorted({k for k in list(out["counters"]) + list(out["kernels"]) if "raster_kernel" in k})

@@ -64,7 +64,7 @@ elif [ "$PART" = B ]; then
   bash tools/pack_profile.sh ${TAG}_sa
   bash tools/profile_sa_late.sh ${TAG}_sa_late > gpurun_out/${TAG}_sa_late_profile.log 2>&1; ok $? profile_sa_late
   show gpurun_out/prof_${TAG}_sa_late/summary.json
-  bash tools/pack_profile.sh ${TAG}_sa_late
+  PROF_RASTER_GRID=2097152 bash tools/pack_profile.sh ${TAG}_sa_late
 else
   echo "part must be A or B"; exit 2
 fi
