@@ -170,10 +170,6 @@ struct DevCtx {
     // host-API staging
     DevBuf gen, out, target, mask;
     PinBuf h_out;                  // the fitness scalars (render and genomes go straight to / from the caller)
-    // host-API pipeline (fitness_one_device_speculative): the genome upload is split
-    // in two on `stream`; each part is evaluated on its own stream as soon as it lands
-    hipStream_t pipe[2] = {nullptr, nullptr};
-    hipEvent_t up[2] = {nullptr, nullptr}, fin[2] = {nullptr, nullptr};
     uint64_t target_key = 0, mask_key = 0;
     size_t target_bytes = 0, mask_bytes = 0;
 };
@@ -410,6 +406,7 @@ int check_dims(int64_t B, int32_t N, int32_t C, int32_t H, int32_t W) {
     if (C < 9) return fail(GGS_EINVAL, "expected at least 9 genome cols, got C=%d (render.py:223)", C);
     if (H < 1 || W < 1) return fail(GGS_EINVAL, "H=%d, W=%d must be >= 1", H, W);
     // the raster's cull list holds 32-bit byte offsets of 64-B records: N * 64 < 2^31
+    // (N <= 512 launches pack the visit's control into the offset's free bits)
     if ((int64_t)N * (int64_t)sizeof(SplatRec) >= ((int64_t)1 << 31))
         return fail(GGS_EINVAL, "N=%d splats per candidate exceeds the limit %lld", N,
                     (long long)(((int64_t)1 << 31) / (int64_t)sizeof(SplatRec) - 1));
@@ -594,11 +591,6 @@ void ggs_shutdown(void) {
             if (b->p) (void)hipFree(b->p);
         for (PinBuf* b : {&c->h_out})
             if (b->p) (void)hipHostFree(b->p);
-        for (int k = 0; k < 2; ++k) {
-            if (c->pipe[k]) (void)hipStreamDestroy(c->pipe[k]);
-            if (c->up[k]) (void)hipEventDestroy(c->up[k]);
-            if (c->fin[k]) (void)hipEventDestroy(c->fin[k]);
-        }
         (void)hipStreamDestroy(c->stream);
     }
     g_ctx.clear();
@@ -720,33 +712,6 @@ uint64_t host_plan_key(uint64_t tkey, uint64_t mkey, float boost_beta, int mode,
              ((uint64_t)mode << 2) ^ ((uint64_t)H << 40) ^ ((uint64_t)W << 20)) & ~(1ull << 63)) | 1;
 }
 
-// The host API's two-part pipeline.  A dependent caller (a GA generation) waits
-// for each call, so with one stream the whole genome upload (1.18 MB at
-// 512^2/256/128: ~26 us of PCIe) ran before any kernel.  Split: the first part is
-// the largest number of candidates whose raster fills at most two of the three
-// wave slots per SIMD (it starts after a short upload and leaves room for the
-// second part's prep), the second part is uploaded meanwhile and evaluated on its
-// own stream, its raster overlapping the first's tail.  Returns the first part's
-// size, or 0: one part (single-round batches, or GGS_HOST_PIPE=0).  A candidate's
-// bits never depend on the launch it is in.
-int64_t pipeline_split(const DevCtx* c, int64_t B, int H, int W) {
-    const char* v = getenv("GGS_HOST_PIPE");
-    if (v && atoi(v) == 0) return 0;
-    const int64_t strips = 4 * (int64_t)raster_tiles(H, W, nullptr);
-    if (c->simds <= 0 || B * strips <= 3 * (int64_t)c->simds) return 0;
-    const int64_t b0 = std::max<int64_t>(1, (2 * (int64_t)c->simds) / strips);
-    return b0 < B ? b0 : 0;
-}
-
-int ensure_pipe(DevCtx* c) {
-    for (int k = 0; k < 2; ++k) {
-        if (!c->pipe[k]) GGS_HIP(hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking));
-        if (!c->up[k]) GGS_HIP(hipEventCreateWithFlags(&c->up[k], hipEventDisableTiming));
-        if (!c->fin[k]) GGS_HIP(hipEventCreateWithFlags(&c->fin[k], hipEventDisableTiming));
-    }
-    return GGS_OK;
-}
-
 // One device, host arrays in and out.  The content hashes of target and mask
 // (4 MB at 512^2: ~0.2 ms on one core) decide whether the device copies cached
 // from an earlier call are still right.  A GA passes the same arrays every
@@ -773,50 +738,21 @@ int fitness_one_device_speculative(DevCtx* c, const float* genomes_axes, int64_t
     GGS_HIP(hipStreamSynchronize(st));  // the previous call's work is done with c->gen
     StreamDrain drain;                  // after the context lock: drained on every return
     drain.add(c->dev, st);
-    const int64_t b1 = pipeline_split(c, B, H, W);
-    if (b1 > 0 && (rc = ensure_pipe(c))) return rc;
     // straight from the caller's (pageable) array: the runtime's own staged copy
     // beat a memcpy into our pinned buffer + its upload by ~25 us per call at
     // 512^2/256/128 (1.18 MB: 240 -> 215 us per call; docs/EXPERIMENTS.md §15).  The
     // array stays valid for the whole call, which syncs before returning.
-    const size_t rowb = sizeof(float) * (size_t)N * C;
-    if (b1 > 0) {                       // two parts, each announced by its event
-        GGS_HIP(hipMemcpyAsync(c->gen.p, genomes_axes, rowb * b1, hipMemcpyHostToDevice, st));
-        GGS_HIP(hipEventRecord(c->up[0], st));
-        GGS_HIP(hipMemcpyAsync((char*)c->gen.p + rowb * b1, (const char*)genomes_axes + rowb * b1,
-                               rowb * (B - b1), hipMemcpyHostToDevice, st));
-        GGS_HIP(hipEventRecord(c->up[1], st));
-    } else if (gbytes) {
-        GGS_HIP(hipMemcpyAsync(c->gen.p, genomes_axes, gbytes, hipMemcpyHostToDevice, st));
-    }
+    if (gbytes) GGS_HIP(hipMemcpyAsync(c->gen.p, genomes_axes, gbytes, hipMemcpyHostToDevice, st));
     const uint64_t mkey_c = mask_hw ? c->mask_key : 0;
-    // (pipe = false: everything on `st`, after the uploads queued there — the redo
-    // below, whose new target / mask are uploaded on `st`)
-    auto evaluate = [&](uint64_t tk, uint64_t mk, bool pipe) {
-        const uint64_t key = host_plan_key(tk, mk, boost_beta, mode, H, W);
-        if (pipe && b1 > 0) {
-            for (int k = 0; k < 2; ++k) {
-                const int64_t o = k ? b1 : 0, n = k ? B - b1 : b1;
-                hipStream_t ps = c->pipe[k];
-                drain.add(c->dev, ps);
-                GGS_HIP(hipStreamWaitEvent(ps, c->up[k], 0));
-                int r = run_fitness(c, ps, (const float*)((const char*)c->gen.p + rowb * o), n, N, C,
-                                    (const float*)c->target.p, mask_hw ? (const float*)c->mask.p : nullptr, mode,
-                                    boost_beta, H, W, k_sigma, (float*)c->out.p + o, key);
-                if (r) return r;
-                GGS_HIP(hipEventRecord(c->fin[k], ps));
-                GGS_HIP(hipStreamWaitEvent(st, c->fin[k], 0));
-            }
-        } else {
-            int r = run_fitness(c, st, (const float*)c->gen.p, B, N, C, (const float*)c->target.p,
-                                mask_hw ? (const float*)c->mask.p : nullptr, mode, boost_beta, H, W, k_sigma,
-                                (float*)c->out.p, key);
-            if (r) return r;
-        }
+    auto evaluate = [&](uint64_t tk, uint64_t mk) {
+        int r = run_fitness(c, st, (const float*)c->gen.p, B, N, C, (const float*)c->target.p,
+                            mask_hw ? (const float*)c->mask.p : nullptr, mode, boost_beta, H, W, k_sigma,
+                            (float*)c->out.p, host_plan_key(tk, mk, boost_beta, mode, H, W));
+        if (r) return r;
         GGS_HIP(hipMemcpyAsync(c->h_out.p, c->out.p, sizeof(float) * (size_t)B, hipMemcpyDeviceToHost, st));
         return GGS_OK;
     };
-    if ((rc = evaluate(c->target_key, mkey_c, true))) return rc;
+    if ((rc = evaluate(c->target_key, mkey_c))) return rc;
     if (inject_fail_after(1)) return fail(GGS_EHIP, "injected failure after device 1's work (test hook)");
     const uint64_t tkey = hash_bytes(target_hw3, tbytes);      // while the GPU runs
     const uint64_t mkey = mask_hw ? hash_bytes(mask_hw, mbytes) : 0;
@@ -831,7 +767,7 @@ int fitness_one_device_speculative(DevCtx* c, const float* genomes_axes, int64_t
             GGS_HIP(hipMemcpyAsync(c->mask.p, mask_hw, mbytes, hipMemcpyHostToDevice, st));
             c->mask_key = mkey;
         }
-        if ((rc = evaluate(tkey, mkey, false))) return rc;     // the first evaluation has drained
+        if ((rc = evaluate(tkey, mkey))) return rc;
         if ((rc = drain.drain())) return rc;
     }
     memcpy(out_B, c->h_out.p, sizeof(float) * (size_t)B);

@@ -164,6 +164,27 @@ constexpr int SAT_BATCH = GGS_SAT_BATCH;
 
 __device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// A cull-list word of the instances without the saturation check (N <= 512) and
+// without the folded finalize: the visit's scalar control, formed by the cull (one
+// lane per splat, VALU) instead of per visit (SALU) — the record byte offset i * 64 (bits 6-25) with, in its
+// free bits, kB (0-4: the strip's last row pair the AABB reaches, NPK when it
+// reaches past the tile), "starts at or above the tile" (5), kA (26-29: the first
+// row pair) and "the AABB cuts the strip's 16 columns" (31).  The same integer
+// tests on the same bounds, so the same paths: 7 fewer SALU per visit, raster
+// -0.5 % at 512^2/256, -0.25 % at the shipped GA launch; the saturation instances
+// (2048^2 SA: +1.5 %, the longer cull pays the words) keep plain byte offsets
+// (docs/EXPERIMENTS.md §16).
+constexpr unsigned VW_ABOVE = 32u, VW_KA = 26, VW_CLIP = 31, VW_OFFSET = 0x03FFFFC0u;
+__device__ __forceinline__ int visit_word(int i, const int4& bb, int ty0, int sx0) {
+    constexpr int NP = GGS_TILE_H / 8;
+    const int dy0 = bb.z - ty0, dy1 = bb.w - ty0;
+    const unsigned kA = (unsigned)max(dy0, 0) >> 3;
+    const unsigned kB = dy1 >= GGS_TILE_H - 1 ? (unsigned)NP : (unsigned)dy1 >> 3;
+    const unsigned above = dy0 <= 0 ? VW_ABOVE : 0u;
+    const unsigned clip = max(bb.x - sx0, sx0 + 15 - bb.y) > 0 ? (1u << VW_CLIP) : 0u;
+    return (int)(((unsigned)i << 6) | kB | above | (kA << VW_KA) | clip);
+}
+
 // One strip's partial (lane 0).  With the fused finalize: an agent-scope store,
 // written through to the device coherence point, where the candidate's last wave
 // (on any XCD) reads it.  Otherwise a plain store (the finalize launch reads it
@@ -323,6 +344,10 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
               const int* __restrict__ tile_order, const unsigned char* __restrict__ dirty,
               const float* __restrict__ clean, const int* __restrict__ live, int CH, FinFused fin, int simds) {
     constexpr bool DS = GGS_DEPTH_SPLIT && MODE == 1 && !SAT;
+    // cull-list words carry the visit's scalar control (visit_word): the instances
+    // without the saturation check and the folded finalize (in the GA's folded
+    // instance they cost 3 SGPR spills to VGPR lanes; the saturation instances lost 1.5 %)
+    constexpr bool VW = !SAT && !FUSED;
     __shared__ int lists[DS ? 2 : WPB][CAP];   // per-wave strip lists (descending splat index)
 
     const int lane = threadIdx.x & 63;
@@ -482,7 +507,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             /* deeper: reload after the test, into the registers just read */              \
             if (AHEAD > 1) BB = bounds(i - 64 * AHEAD);                                     \
             const uint64_t m = __ballot(hit);                                               \
-            if (hit) list[cnt + __popcll(m & lt_mask)] = i * (int)sizeof(SplatRec);  /* byte offset */ \
+            if (hit) list[cnt + __popcll(m & lt_mask)] =                                    \
+                VW ? visit_word(i, bb, ty0, sx0) : i * (int)sizeof(SplatRec);                \
             cnt += __popcll(m);                                                             \
             base += 64;                                                                     \
         }
@@ -535,8 +561,8 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
         };
 #endif
         int offv = GGS_LIST_AT(min(lane, cnt - 1));
-        // one (splat, strip) visit: cull-list record s -> the strip's accumulators
-        auto visit = [&](const SplatRec& s) __attribute__((always_inline)) {
+        // one (splat, strip) visit: cull-list record s (list word w) -> the strip's accumulators
+        auto visit = [&](const SplatRec& s, const unsigned w) __attribute__((always_inline)) {
 #if GGS_TIMING
             ++n_done;
 #endif
@@ -554,7 +580,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             // The empty asm keeps the compiler from if-converting it back into an
             // unconditional compare + select).  Dead lanes: px = -inf (f = 0; the
             // ratio's clamp keeps their walk at 0, see GGS_RATIO).
-            if (__builtin_expect(max(x0 - sx0, sx0 + 15 - x1) > 0, 0)) {
+            if (__builtin_expect(VW ? (w >> VW_CLIP) != 0 : max(x0 - sx0, sx0 + 15 - x1) > 0, 0)) {
                 const bool inx = (unsigned)(col - x0) <= (unsigned)(x1 - x0);
                 px = inx ? px : -__builtin_inff();
                 asm volatile("" : "+v"(px));
@@ -566,7 +592,9 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             // first / last group pair; kB = NPK: the splat reaches past the tile's
             // last row, so the walk's last pair needs no bottom-row mask (about half
             // the partial visits: 4 VALU fewer each, the same bits)
-            const int kA = gA >> 1, kB = dy1 >= TILE_H - 1 ? NPK : gB >> 1;
+            // the visit's scalar control: from the list word, or (saturation instances) here
+            const int kA = VW ? (int)(w >> VW_KA) & 15 : gA >> 1;
+            const int kB = VW ? (int)w & 31 : (dy1 >= TILE_H - 1 ? NPK : gB >> 1);
             f2_t F2, R2;                                       // row recurrence: f, ratio
             // First pair: exact exponent; keeps the unmasked f as the recurrence
             // seed and, when more pairs follow, the ratio 2^d to the next pair.
@@ -577,7 +605,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             // them on the bench population) need no row mask and no walk exit
             // test: one straight-line block, the same arithmetic as the general
             // walk (kA = 0, kB = NPK-1, all-ones masks), so the same bits.
-            if (max(dy0, TILE_H - 1 - dy1) <= 0) {            // y0 <= ty0 and y1 >= ty0 + 127
+            if (VW ? (w & 63u) == (VW_ABOVE | NPK) : max(dy0, TILE_H - 1 - dy1) <= 0) {   // y0 <= ty0, y1 >= ty0 + 127
                 const f2_t e_ = GGS_E1(qyv);
                 F2.x = GGS_EXP2(e_.x);
                 F2.y = GGS_EXP2(e_.y);
@@ -605,7 +633,7 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
             // About half the partial visits start above the tile (the splat began in
             // a tile above): their first pair needs no top-row mask (GGS_FIRST(0)
             // with all-ones masks: the same bits, 4 VALU fewer).
-            if (dy0 <= 0) {
+            if (VW ? (w & VW_ABOVE) != 0 : dy0 <= 0) {        // dy0 <= 0
                 const f2_t e_ = GGS_E1(qyv);
                 F2.x = GGS_EXP2(e_.x);
                 F2.y = GGS_EXP2(e_.y);
@@ -768,20 +796,25 @@ raster_kernel(const SplatRec* __restrict__ recs, const int4* __restrict__ bnds, 
 #undef rows_upto
         // two records in alternating SGPR sets: the next record is loaded into
         // the set the finished visit used, so no register rotation at the latch
-        auto load_at = [&](int jj) __attribute__((always_inline)) {
-            return *reinterpret_cast<const SplatRec*>(
-                cbase + (unsigned)__builtin_amdgcn_readlane(offv, jj & 63));
+        auto word_at = [&](int jj) __attribute__((always_inline)) {
+            return (unsigned)__builtin_amdgcn_readlane(offv, jj & 63);
         };
-        SplatRec ra = load_at(0);
+        auto load_at = [&](unsigned w) __attribute__((always_inline)) {
+            return *reinterpret_cast<const SplatRec*>(cbase + (VW ? (w & VW_OFFSET) : w));
+        };
+        unsigned wa = word_at(0);
+        SplatRec ra = load_at(wa);
         int jr = 63;                  // last j before the next 64 offsets are needed
         for (int j = 0;;) {
             if (__builtin_expect(j == jr, 0)) { jr += 64; offv = GGS_LIST_AT(min(j + 1 + lane, cnt - 1)); }
-            const SplatRec rb = load_at(j + 1);
-            visit(ra);
+            const unsigned wb = word_at(j + 1);
+            const SplatRec rb = load_at(wb);
+            visit(ra, wa);
             if (++j >= cnt) break;
             if (__builtin_expect(j == jr, 0)) { jr += 64; offv = GGS_LIST_AT(min(j + 1 + lane, cnt - 1)); }
-            ra = load_at(j + 1);
-            visit(rb);
+            wa = word_at(j + 1);
+            ra = load_at(wa);
+            visit(rb, wb);
             if (++j >= cnt) break;
 #if GGS_SATURATE
             // (strips reaching past the image keep T = 1 outside it: never cut)

@@ -484,8 +484,7 @@ def test_target_cache_speculation_in_place_and_mode_changes(full_size, n):
     caller's arrays (ggs_capi.cpp fitness_one_device_speculative): every result
     must equal a fresh evaluation of the arrays as they are at the call — after
     in-place edits of the same buffers, a mask-only change, a mode change and a
-    switch to no mask.  n = 128: the two-part pipeline (upload split, parts on
-    their own streams), whose redo after a content change runs on one stream."""
+    switch to no mask (n = 128: the bench's batch, a multi-round launch)."""
     pop, tgt, mask, H, W = full_size
     P = pop[:n]
     t, m = tgt.copy(), mask.copy()
@@ -520,27 +519,6 @@ def test_target_cache_speculation_in_place_and_mode_changes(full_size, n):
     e = ggs.fitness(P, t, H, W, 3.0)                                                  # no mask
     np.testing.assert_array_equal(e, fresh(t, None))
     np.testing.assert_array_equal(ggs.fitness(P, t, H, W, 3.0, weight_mask=m), c)
-
-
-def test_host_pipeline_equals_one_stream(full_size, monkeypatch):
-    """The host API's two-part pipeline (GGS_HOST_PIPE, read per call) returns the
-    one-stream evaluation's bits, call after call, with the genome array edited in
-    place between calls (the upload happens inside each call)."""
-    pop, tgt, mask, H, W = full_size
-    g = pop.copy()
-    outs = {}
-    for pipe in ("1", "0"):
-        monkeypatch.setenv("GGS_HOST_PIPE", pipe)
-        g[:] = pop
-        r = [ggs.fitness(g, tgt, H, W, 3.0, weight_mask=mask)]
-        g[:, :, 5:8] = 255.0 - g[:, :, 5:8]
-        r.append(ggs.fitness(g, tgt, H, W, 3.0, weight_mask=mask))
-        r.append(ggs.fitness(g[:70], tgt, H, W, 3.0, weight_mask=mask))
-        outs[pipe] = r
-    for a, b in zip(outs["1"], outs["0"]):
-        np.testing.assert_array_equal(a, b)
-    assert (outs["1"][0] != outs["1"][1]).any()
-    np.testing.assert_array_equal(outs["1"][2], outs["1"][1][:70])
 
 
 def test_full_size_two_streams_concurrent_bit_identical(full_size):
