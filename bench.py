@@ -544,6 +544,9 @@ def main(argv=None):
 
 def run(args, world, rank, local_rank, distributed):
     global H, W, N_SPLATS, POP
+    # no torch in this process: /opt/rocm's HIP runtime and RCCL.  Set before anything
+    # imports ggs (launch_key below does: the round-5 line ran on torch's runtime)
+    os.environ.setdefault("GGS_HIP_RUNTIME", "system")
     H, N_SPLATS, pop_cfg, scaling = CONFIGS[args.config]
     W = H
     if scaling == "strong":                      # configs[3]: one population split over the ranks
@@ -575,9 +578,14 @@ def run(args, world, rank, local_rank, distributed):
                          f"hardware queue and serialise one rank's gathers behind another's")
     wd = Watchdog(rank, world, launch_key())
     wd.arm("set-up (device, target plan, communicators, first barrier)", args.watchdog_init_s)
-    os.environ.setdefault("GGS_HIP_RUNTIME", "system")   # no torch in this process: /opt/rocm's HIP
     import ggs
     from ggs import hip
+    lib_mod = getattr(ggs, "_lib", None)
+    if os.environ.get("GGS_HIP_RUNTIME") == "system" and hasattr(lib_mod, "rocm_lib_dir"):
+        hip_path = ggs.runtime_info().get("hip") or ""
+        if os.path.dirname(hip_path) != lib_mod.rocm_lib_dir():
+            raise SystemExit(f"bench.py: GGS_HIP_RUNTIME=system but libggs is bound to {hip_path!r} "
+                             f"(ggs was imported before the setting took effect)")
 
     n_dev = ggs.ensure_init()
     if local_rank >= n_dev:
