@@ -248,6 +248,40 @@ def test_fitness_matches_reference_golden(case):
     np.testing.assert_allclose(chunked, d[f"{case}__pop_chunk2"], rtol=FIT_RTOL)
 
 
+def test_fitness_edge_inputs():
+    """fitness.py:7-47 at the edges: an empty batch, candidates without splats (the
+    background alone), an all-zero weight mask (weighted: 0 / (0 + 1e-12) = 0), mask
+    values outside [0, 1] (boost clamps them, fitness.py:24), a one-pixel canvas and
+    one-row / one-column canvases — against the oracle in every mode."""
+    rng = np.random.default_rng(77)
+    H, W = 33, 47
+    tgt = rng.uniform(0, 1, (H, W, 3)).astype(np.float32)
+    mask = rng.uniform(0, 1, (H, W)).astype(np.float32)
+    modes = ({}, {"weight_mask": mask}, {"weight_mask": mask, "boost_only": True})
+    assert np.asarray(ggs.fitness(np.zeros((0, 5, 9), np.float32), tgt, H, W, 3.0)).shape == (0,)
+    assert list(ggs.fitness_population([], tgt, H, W, 3.0, weight_mask=mask)) == []
+    none = np.zeros((2, 0, 9), np.float32)
+    for kw in modes:
+        np.testing.assert_allclose(ggs.fitness(none, tgt, H, W, 3.0, **kw),
+                                   O.fitness_many(list(none), tgt, H, W, 3.0, **kw), rtol=FIT_RTOL)
+    pop = O.synthetic_population(3, 40, H, W, seed=8)
+    zero = np.zeros((H, W), np.float32)
+    np.testing.assert_array_equal(ggs.fitness(pop, tgt, H, W, 3.0, weight_mask=zero), np.zeros(3, np.float32))
+    wild = rng.uniform(-2, 3, (H, W)).astype(np.float32)
+    for kw in ({"weight_mask": zero, "boost_only": True}, {"weight_mask": wild, "boost_only": True}):
+        np.testing.assert_allclose(ggs.fitness(pop, tgt, H, W, 3.0, **kw),
+                                   O.fitness_many(list(pop), tgt, H, W, 3.0, **kw), rtol=FIT_RTOL)
+    for h, w in ((1, 1), (1, 96), (96, 1)):
+        t = rng.uniform(0, 1, (h, w, 3)).astype(np.float32)
+        m = rng.uniform(0, 1, (h, w)).astype(np.float32)
+        p = O.synthetic_population(2, 9, h, w, seed=h * 1000 + w)
+        np.testing.assert_allclose(ggs.render(O.genome_to_renderer_batched(p), h, w),
+                                   O.render(O.genome_to_renderer_batched(p), h, w), atol=IMG_TOL, rtol=0)
+        for kw in ({}, {"weight_mask": m}, {"weight_mask": m, "boost_only": True}):
+            np.testing.assert_allclose(ggs.fitness(p, t, h, w, 3.0, **kw),
+                                       O.fitness_many(list(p), t, h, w, 3.0, **kw), rtol=FIT_RTOL)
+
+
 def test_fitness_vs_oracle_512():
     H = W = 512
     pop = O.synthetic_population(4, 256, H, W, seed=21)
