@@ -47,6 +47,9 @@ def _problem(H, W, seed):
     (32, 32, 8, 2, 5, 2, 1, 0.3, 0.01, False, 3),      # N = 2, rare mutation -> fallbacks
     (24, 24, 6, 1, 3, 2, 0, 0.5, 0.5, False, 4),       # N = 1: no swap; elite_k 0 -> 1
     (16, 16, 600, 3, 2, 3, 25, 0.5, 0.1, False, 5),    # P > 512: bitonic survivors path
+    (24, 24, 8, 20, 3, 2, 8, 0.5, 0.2, False, 10),     # elite_k == P: no offspring survive (algorithm.py:140)
+    (24, 24, 10, 40, 3, 1, 2, 0.5, 0.2, True, 11),     # tour_k 1: the tournament is one random pick
+    (24, 24, 12, 30, 2, 40, 2, 0.5, 0.2, False, 12),   # 2 tour_k > 64: the per-candidate tournament loop
 ])
 @pytest.mark.parametrize("chunk", [2, 8])   # 8 >= G: one run, every later generation a fused breed
 def test_device_ga_matches_host_ga_with_same_draws(H, W, P, N, G, tour_k, elite_k, cxpb, mutpb,
