@@ -393,6 +393,29 @@ def test_device_loop_matches_host_loop(H, W, N, tries, spec, inc, iters):
         assert 0 < ds["stats"]["accepted"] and ds["stats"]["evaluated"] >= iters * tries
 
 
+@pytest.mark.parametrize("tries,temp0", [(1, 5e-2), (4, 0.0)])
+def test_device_loop_edge_schedules_match_host_loop(tries, temp0):
+    """One try per iteration (every round is one neighbour of one iteration), and
+    T0 = 0: the cosine schedule floors T at 1e-12 (annealing.py:37), so a rise dE
+    of a float32 energy never passes the Metropolis test (annealing.py:133-145):
+    the current energy never rises and equals the best curve."""
+    H = W = 48
+    N = 24
+    target, _, _ = _problem(H, W, 13)
+    init = ga.new_population(1, N, H, W, MIN_S, MAX_S, np.random.default_rng(13))[0]
+    kw = dict(tries_per_iter=tries, init_individual=init, iterations=10, temp0=temp0, backend="device",
+              seed=5)
+    hb, hf, hs = _sa(target, H, W, N, loop="host", **kw)
+    db, df, ds = _sa(target, H, W, N, loop="device", chunk=4, **kw)
+    np.testing.assert_array_equal(db, hb)
+    np.testing.assert_array_equal(ds["current"], hs["current"])
+    assert df == hf and ds["curves"] == hs["curves"] and ds["current_fit"] == hs["current_fit"]
+    assert ds["stats"]["tries"] == 10 * tries
+    if temp0 == 0.0:
+        cur = ds["curves"]["current"]
+        assert all(y <= x for x, y in zip(cur, cur[1:])) and cur == ds["curves"]["best"]
+
+
 def test_device_loop_width_invariant_low_temperature():
     """Rare acceptances: rounds span several iterations (width up to the cap);
     the trajectory does not depend on the width or the chunking."""
